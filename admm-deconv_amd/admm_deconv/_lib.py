@@ -1,0 +1,95 @@
+"""ctypes binding of the C ABI declared in include/admm_deconv.h.
+
+The product path: every solve goes through `libadmm_deconv.so` (hand-written HIP for gfx950).
+There is no CPU or PyTorch fallback -- if the library is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # .../admm-deconv_amd
+LIB_PATH = os.path.join(PKG_ROOT, "libadmm_deconv.so")
+
+ADMM_OK = 0
+ADMM_E_INVALID = -1
+ADMM_E_UNSUPPORTED = -2
+ADMM_E_WORKSPACE = -3
+ADMM_E_HIP = -4
+
+K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM = range(6)
+KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
+                  K_FINAL: "final", K_NORM: "norm"}
+
+# Every symbol include/admm_deconv.h declares (checked by tests/test_capi.py).
+EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "admm_tvd_forward_f32",
+           "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
+
+
+class AdmmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"admm_deconv error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree HIP library (built by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(there is deliberately no CPU fallback)")
+    try:
+        import torch  # noqa: F401  -- share torch's HIP runtime (same SONAME) when torch is in use
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    c_int, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+    L.admm_abi_version.restype = c_int
+    L.admm_abi_version.argtypes = []
+    L.admm_last_error.restype = ctypes.c_char_p
+    L.admm_last_error.argtypes = []
+    L.admm_tvd_workspace_bytes.restype = c_int
+    L.admm_tvd_workspace_bytes.argtypes = [c_int] * 7 + [ctypes.POINTER(c_size_t)]
+    L.admm_tvd_forward_f32.restype = c_int
+    L.admm_tvd_forward_f32.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                       c_float, c_float, c_int, c_int, c_void_p, c_size_t, c_void_p]
+    L.admm_profile_enable.restype = c_int
+    L.admm_profile_enable.argtypes = [c_int]
+    L.admm_profile_reset.restype = c_int
+    L.admm_profile_reset.argtypes = []
+    L.admm_profile_get.restype = c_int
+    L.admm_profile_get.argtypes = [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != ADMM_OK:
+        raise AdmmError(rc, load().admm_last_error().decode(errors="replace"))
+    return rc
+
+
+def workspace_bytes(M, N, P, B, kh, kw, iso):
+    out = ctypes.c_size_t(0)
+    check(load().admm_tvd_workspace_bytes(M, N, P, B, kh, kw, int(bool(iso)), ctypes.byref(out)))
+    return out.value
+
+
+def profile_enable(on=True):
+    check(load().admm_profile_enable(int(bool(on))))
+
+
+def profile_reset():
+    check(load().admm_profile_reset())
+
+
+def profile_get(cls):
+    ms = ctypes.c_double(0)
+    n = ctypes.c_longlong(0)
+    check(load().admm_profile_get(int(cls), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value

@@ -1,0 +1,89 @@
+/*
+ * admm_deconv.h -- C ABI of the MI355X-native ADMM TV-deconvolution solve.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   tvd_fft(y, λ, ρ, h, isotropic=false, maxit=100)          /root/reference/src/ops/ops.jl:181-188
+ * whose two bodies are tvd_fft_cpu (ops.jl:17-96) and tvd_fft_gpu (ops.jl:99-178).  The
+ * reference reaches it from the Flux layer forward `(d::Admm)(x)` (src/layers/deconv_admm.jl:215-225),
+ * which clamps λ, ρ and the PSF first; callers of this ABI pass the already-clamped fp32 values.
+ * The Julia `ccall` binding a maintainer would add, and the Python ctypes binding this repo uses,
+ * are shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every array pointer is a DEVICE pointer owned by the caller.  Layout is the reference's
+ *    column-major Julia array (M,N,P,B) == C `float[B][P][N][M]` (dim1 = M contiguous).
+ *    The PSF h is Julia (kh,kw,1,1) == C `float[kw][kh]`; kh == kw == 0 (or h == NULL) is the
+ *    reference's empty PSF (`isempty(h)` -> H = identity, ops.jl:22-23,67-69).
+ *  - The library allocates nothing in the solve: the caller supplies a device workspace of at
+ *    least admm_tvd_workspace_bytes() bytes (256-byte aligned).  Work is enqueued on `stream`
+ *    (a hipStream_t, NULL = default stream) and is asynchronous, like CUDA.jl's task-local stream.
+ *    `y` is never modified; the result goes to `x_out` (the reference returns a new array).
+ *  - Return value: 0 on success, a negative ADMM_E* code otherwise; admm_last_error() gives a
+ *    thread-local message for the last failing call.
+ *  - Supported shapes (this build): M, N powers of two with 4 <= M <= 1024, 2 <= N <= 1024;
+ *    kh <= M, kw <= N, kh*kw <= 4096.  Other shapes return ADMM_E_UNSUPPORTED (the reference accepts any
+ *    M x N through FFTW/CUFFT; non-power-of-two sizes are a listed next step).
+ */
+#ifndef ADMM_DECONV_H
+#define ADMM_DECONV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADMM_ABI_VERSION 1
+
+enum {
+    ADMM_OK = 0,
+    ADMM_E_INVALID = -1,      /* bad argument (null pointer, negative size, non-finite λ/ρ) */
+    ADMM_E_UNSUPPORTED = -2,  /* shape/option outside this build's support matrix           */
+    ADMM_E_WORKSPACE = -3,    /* workspace too small or misaligned                          */
+    ADMM_E_HIP = -4           /* a HIP runtime call failed (message has hipGetErrorString)   */
+};
+
+/* Kernel classes, for the optional per-kernel profiler (admm_profile_*). */
+enum {
+    ADMM_K_SETUP = 0,   /* twiddles + C spectrum (ops.jl:22-37)                                 */
+    ADMM_K_PREP = 1,    /* H^T y (ops.jl:71-81) + first line rFFT                                */
+    ADMM_K_COLUMN = 2,  /* column pass: FFT along dim2, x C, IFFT along dim2 (ops.jl:86 part)    */
+    ADMM_K_LINE = 3,    /* line pass: irFFT dim1 -> D -> prox -> dual -> D^T -> +H^T y -> rFFT   */
+    ADMM_K_FINAL = 4,   /* last irFFT along dim1, writes x                                       */
+    ADMM_K_NORM = 5,    /* isotropic only: pixelnorm over the batch (ops.jl:6)                   */
+    ADMM_K_COUNT = 6
+};
+
+/* ABI version of the loaded library (== ADMM_ABI_VERSION it was built with). */
+int admm_abi_version(void);
+
+/* Thread-local message describing the most recent failure ("" if none). */
+const char* admm_last_error(void);
+
+/* Workspace size for one tvd_fft call of this shape.  Replaces the allocations
+ * tvd_fft_gpu makes internally (ops.jl:104-131, fresh temporaries every iteration). */
+int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso,
+                             size_t* out_bytes);
+
+/* The solve.  Replaces tvd_fft(y, λ, ρ, h, isotropic, maxit) (ops.jl:181-188) for device
+ * arrays: returns x after `maxit` ADMM iterations of
+ *   x = irfft(C .* rfft(H^T y + ρ D^T(z-u))),  z = prox(Dx+u, λ/ρ),  u = u + Dx - z
+ * with prox = ST (iso == 0, ops.jl:9) or BT (iso == 1, ops.jl:10; couples the whole batch).
+ * maxit == 0 returns zeros (the reference's initial x, ops.jl:46). */
+int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B,
+                         const float* h, int kh, int kw, float lambda, float rho, int iso,
+                         int maxit, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
+ * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises
+ * the stream before returning.  admm_profile_get returns the accumulated device time (ms) and
+ * launch count of one ADMM_K_* class since the last reset. */
+int admm_profile_enable(int on);
+int admm_profile_reset(void);
+int admm_profile_get(int kernel_class, double* total_ms, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADMM_DECONV_H */

@@ -1,0 +1,97 @@
+"""GPU parity: the HIP path (through the C ABI) against the fp64 CPU oracle on identical fp32 inputs.
+
+Oracle: oracle/oracle_np.py (restatement of /root/reference/src/ops/ops.jl:17-96, parity unpinned
+against Julia itself -- see DESIGN.md).  Tolerance: tests/parity.py."""
+import numpy as np
+import pytest
+import torch
+
+import admm_deconv
+import oracle_np
+from admm_deconv import synth
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def run_gpu(dev, y, lam, rho, h, iso, K):
+    ht = None if h is None else torch.from_numpy(np.ascontiguousarray(h, np.float32)).to(dev)
+    x = admm_deconv.tvd_fft(torch.from_numpy(np.ascontiguousarray(y, np.float32)).to(dev), lam, rho, ht, iso, K)
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+def run_oracle(y, lam, rho, h, iso, K):
+    return oracle_np.to_c(oracle_np.tvd_fft_literal(oracle_np.from_c(np.asarray(y, np.float64)), np.float32(lam),
+                                                    np.float32(rho), oracle_np.psf_from_c(h), iso, K))
+
+
+CASES = [
+    # (B, P, N, M, psf, lam, rho, K)
+    (1, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 10),     # BASELINE c1
+    (2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25),  # c2 slices
+    (3, 1, 16, 8, ("rand", 3, 2), 0.05, 0.3, 5),
+    (2, 1, 32, 64, ("rand", 10, 10), 0.01, 0.05, 7),          # even PSF (net_build.jl:155)
+    (1, 2, 64, 32, ("rand", 4, 9), 0.02, 0.1, 4),             # asymmetric PSF
+    (2, 3, 64, 64, None, 0.05, 0.02, 12),                      # empty PSF denoiser (F2), RGB
+    (1, 1, 2, 4, None, 0.1, 0.5, 3),                           # smallest supported
+    (1, 1, 1024, 16, ("gauss", 5, 1.0), 0.0041, 0.021, 3),
+    (1, 1, 16, 1024, ("gauss", 5, 1.0), 0.0041, 0.021, 3),
+    (1, 1, 512, 512, ("gauss", 15, 2.5), 0.0041, 0.021, 4),
+    (2, 1, 128, 128, ("box",), 0.0041, 0.021, 100),            # reference test PSF, default maxit
+    (1, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 1),
+    (1, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 2),
+]
+
+
+def make_psf(spec, rng):
+    if spec is None:
+        return None
+    if spec[0] == "gauss":
+        return synth.gaussian_psf(spec[1], spec[2])
+    if spec[0] == "box":
+        return synth.box_psf_row(7)
+    kh, kw = spec[1], spec[2]
+    h = rng.random((kw, kh)).astype(np.float32)
+    return (h / h.sum()).astype(np.float32)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}" for c in CASES])
+def test_parity_vs_oracle(dev, case):
+    B, P, N, M, psf, lam, rho, K = case
+    rng = np.random.default_rng(B * 1000 + N + M + K)
+    h = make_psf(psf, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=7)
+    got = run_gpu(dev, y, lam, rho, h, False, K)
+    ref = run_oracle(y, lam, rho, h, False, K)
+    assert_parity(got, ref, what=str(case))
+
+
+def test_maxit_zero_returns_zeros(dev):
+    y = np.random.default_rng(0).random((2, 1, 16, 16)).astype(np.float32)
+    got = run_gpu(dev, y, 0.01, 0.1, None, False, 0)
+    assert np.all(got == 0)
+
+
+def test_input_not_modified_and_deterministic(dev):
+    h = synth.gaussian_psf(7, 1.5)
+    y = synth.make_batch(4, 64, 64, h)
+    yt = torch.from_numpy(y).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    a = admm_deconv.tvd_fft(yt, 0.0041, 0.021, ht, False, 8)
+    b = admm_deconv.tvd_fft(yt, 0.0041, 0.021, ht, False, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), "solve must be bitwise deterministic"
+    assert np.array_equal(yt.cpu().numpy(), y), "y must not be modified"
+
+
+def test_batch_sharding_invariance(dev):
+    """Aniso planes are independent (ops.jl:168-173): solving any sub-batch gives bitwise the same planes."""
+    h = synth.gaussian_psf(15, 2.5)
+    y = torch.from_numpy(synth.make_batch(8, 256, 256, h)).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    full = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 6)
+    part = torch.cat([admm_deconv.tvd_fft(y[i:i + 3].contiguous(), 0.0041, 0.021, ht, False, 6) for i in (0, 3)]
+                     + [admm_deconv.tvd_fft(y[6:].contiguous(), 0.0041, 0.021, ht, False, 6)])
+    torch.cuda.synchronize()
+    assert torch.equal(full, part)
