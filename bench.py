@@ -1,0 +1,223 @@
+"""Benchmark: ADMM TV-deconvolution images/s at 256x256, K=25 (BASELINE.json metric, config c2).
+
+One "step" = one full tvd_fft solve (src/ops/ops.jl:181 semantics) of a batch of 512 synthetic
+Gaussian-blurred 256x256 images (15x15 PSF, lambda 0.0041, rho 0.021, K = 25, anisotropic) that is
+already resident in HBM, through the HIP library's C ABI.  With N ranks (torchrun, one process per
+GPU) every rank solves its own 512-image shard (weak scaling, no data-path collective; --gather adds
+the RCCL gather of all outputs to rank 0 inside the timed region).
+
+Prints ONE JSON line on rank 0.  Besides the driver's keys it carries
+  roofline      -- dominant kernel: algorithmic bytes per launch / measured avg launch duration
+                   (hipEvents on the launch stream, via the library profiler) vs 8 TB/s HBM peak;
+                   `traffic` = PMC-measured HBM bytes per launch from profiles/ when available.
+  cpu_baseline  -- the C restatement of the reference CPU solve (oracle/admm_oracle.c, fp32, OpenMP)
+                   timed on this host on a bounded sample of the same workload (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "admm-deconv_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import admm_deconv  # noqa: E402
+from admm_deconv import _lib, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def canonical_bytes(M, N, K):
+    """per plane K*[32*(M/2+1)*N + 20*M*N] + 12*M*N."""
+    return K * (32 * (M // 2 + 1) * N + 20 * M * N) + 12 * M * N
+
+
+def kernel_bytes_per_plane(M, N):
+    """Algorithmic bytes per plane for one launch of each kernel class (SURVEY.md s8d split)."""
+    H = M // 2 + 1
+    return {
+        "column": 16 * H * N,                 # read + write the half spectrum
+        "line": 16 * H * N + 20 * M * N,      # spectrum in/out + s in/out (2 ch) + H^T y
+        "prep": 8 * M * N + 8 * H * N,        # y in, H^T y out, spectrum out
+        "final": 8 * H * N + 4 * M * N,       # spectrum in, x out
+    }
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's; c3 -> 2048/N)")
+    ap.add_argument("--gather", action="store_true", help="RCCL gather of all outputs to rank 0 inside the timed region")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic images generated per rank (tiled)")
+    return ap.parse_args()
+
+
+def make_inputs(cfg, B, g0, distinct, dev):
+    psf = synth.gaussian_psf(*cfg["psf"])
+    nd = min(B, distinct)
+    base = synth.make_batch(nd, cfg["M"], cfg["N"], psf, P=cfg["P"], g0=g0)
+    reps = (B + nd - 1) // nd
+    y = np.concatenate([base] * reps)[:B]
+    return torch.from_numpy(np.ascontiguousarray(y)).to(dev), torch.from_numpy(psf).to(dev), psf, base
+
+
+def cpu_baseline(cfg, psf, base, target_s):
+    """Time the C restatement (fp32, OpenMP) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_c
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    n = max(1, min(threads, base.shape[0]))
+    sample = np.ascontiguousarray(base[:n])
+    t0 = time.perf_counter()
+    done = 0
+    runs = 0
+    while True:
+        oracle_c.tvd_fft_c(sample, synth.LAMBDA, synth.RHO, psf, False, cfg["K"], np.float32, nthreads=threads)
+        done += n
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= target_s or runs >= 2000:
+            break
+    return {
+        "value": done / el, "unit": "images/s", "cores": threads, "kind": "port",
+        "sample": f"{runs} x {n} images of {cfg['M']}x{cfg['N']}x{cfg['P']}, K={cfg['K']}, "
+                  f"{cfg['psf'][0]}x{cfg['psf'][0]} PSF, {el:.1f} s wall; C restatement of ops.jl:17-96 "
+                  f"(oracle/admm_oracle.c, fp32, OpenMP over planes)",
+    }
+
+
+def load_traffic(cfg_name, kernel):
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        e = d.get(cfg_name, {}).get(kernel)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    cfg = dict(synth.CONFIGS[args.config])
+    if args.batch:
+        B = args.batch
+    elif args.config == "c3":
+        B = cfg["B"] // world
+    else:
+        B = cfg["B"]
+    M, N, P, K = cfg["M"], cfg["N"], cfg["P"], cfg["K"]
+    y, h, psf_np, base = make_inputs(cfg, B, g0=rank * B, distinct=args.distinct, dev=dev)
+    out = torch.empty_like(y)
+    ws = admm_deconv.Workspace()
+    stream = torch.cuda.current_stream(dev)
+    gathered = None
+    if args.gather and world > 1 and rank == 0:
+        gathered = [torch.empty_like(y) for _ in range(world)]
+
+    def step():
+        admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws, stream=stream)
+        if args.gather and world > 1:
+            dist.gather(out, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    images = B * world * args.steps
+    value = images / el
+    ms_per_step = 1000.0 * el / max(args.steps, 1)
+
+    # ---- per-kernel timing (separate instrumented solve; not part of the timed region) ----
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    reps = 2
+    for _ in range(reps):
+        admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws, stream=stream)
+    _lib.profile_enable(False)
+    planes = B * P
+    kb = kernel_bytes_per_plane(M, N)
+    kernels = {}
+    for cls, name in _lib.KERNEL_CLASSES.items():
+        ms, n = _lib.profile_get(cls)
+        if n == 0:
+            continue
+        avg_ms = ms / n
+        e = {"launches_per_solve": n // reps, "avg_ms": avg_ms, "total_ms_per_solve": ms / reps}
+        if name in kb:
+            e["algorithmic_bytes_per_launch"] = kb[name] * planes
+            e["achieved_GBps"] = kb[name] * planes / (avg_ms * 1e-3) / 1e9
+        kernels[name] = e
+    dom = max((k for k in kernels if k in kb), key=lambda k: kernels[k]["total_ms_per_solve"])
+    traffic = load_traffic(args.config, dom)
+    ach = kernels[dom]["achieved_GBps"]
+    roofline = {
+        "bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
+        "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
+        "whole_solve": {
+            "canonical_bytes": canonical_bytes(M, N, K) * planes,
+            "achieved_GBps": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9, 1),
+            "frac": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        },
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, psf_np, base, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "ADMM deconv images/sec at 256x256 K=25 (% HBM roofline)",
+            "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{args.config}: batch {B}/GPU of {M}x{N}x{P}, {cfg['psf'][0]}x{cfg['psf'][0]} "
+                                   f"Gaussian PSF (sigma {cfg['psf'][1]}), K={K}, anisotropic TV, lambda {synth.LAMBDA}, "
+                                   f"rho {synth.RHO}", "global_batch": B * world, "image": [M, N, P], "K": K,
+                       "parallelism": f"batch-shard x{world}" + (" + RCCL gather" if args.gather and world > 1 else "")},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
