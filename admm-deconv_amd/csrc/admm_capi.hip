@@ -38,7 +38,7 @@ int fail(int code, const char* fmt, ...) {
 bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 struct Layout {
-    size_t twM, twN, C, hty, sA, sB, spec0, spec1, total;
+    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, total;
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
@@ -55,6 +55,7 @@ Layout make_layout(int M, int N, size_t planes, bool psf) {
     L.twM = take((size_t)M * 8);
     L.twN = take((size_t)N * 8);
     L.C = take((size_t)(M / 2 + 1) * N * 4);
+    L.G = psf ? take((size_t)(M / 2 + 1) * N * 8) : 0;
     L.hty = psf ? take(planes * MN * 4) : 0;
     L.sA = take(planes * 2 * MN * 4);
     L.sB = take(planes * 2 * MN * 4);
@@ -65,41 +66,35 @@ Layout make_layout(int M, int N, size_t planes, bool psf) {
 }
 
 // ---- tile-size policy ------------------------------------------------------------------------
-constexpr size_t kLdsBudget = 96 * 1024;
-
-int line_T(int M, int N) {  // largest power-of-two T <= 16 dividing N whose LDS fits
-    int T = N < 16 ? N : 16;
-    while (T > 1) {
-        const size_t L = M / 2;
-        const size_t bytes = (size_t)M * 8 + 2 * (size_t)(T + 2) * L * 8 + (size_t)T * M * 4;
-        if (bytes <= kLdsBudget) break;
-        T >>= 1;
+// T = lines per line-kernel block (power of two dividing N); KB = slots per column-kernel block.
+int line_T(int M, int N) {
+    int pref = M <= 512 ? 8 : 4;
+    if (const char* e = getenv("ADMM_LINE_T")) {
+        int v = atoi(e);
+        if (v == 2 || v == 4 || v == 8 || v == 16) pref = v < pref ? v : pref;
     }
-    return T;
+    return N < pref ? N : pref;
 }
 size_t line_lds(int M, int T) {
     const size_t L = M / 2;
-    return (size_t)M * 8 + 2 * (size_t)(T + 2) * L * 8 + (size_t)T * M * 4;
+    return (size_t)M * 8 + 3 * (size_t)(T + 2) * L * 8;
 }
-size_t final_lds(int M, int T) { return (size_t)M * 8 + 2 * (size_t)T * (M / 2) * 8; }
-size_t prep_lds(int M, int T, int kh, int kw) {
-    size_t b = final_lds(M, T);
-    if (kh > 0) b += (size_t)((kh * kw + 3) & ~3) * 4 + (size_t)(T + kw - 1) * M * 4;
-    return b;
-}
-int prep_T(int M, int N, int kh, int kw) {
-    int T = N < 16 ? N : 16;
-    while (T > 1 && prep_lds(M, T, kh, kw) > kLdsBudget) T >>= 1;
-    return T;
+size_t fwdinv_lds(int M, int T) { return (size_t)M * 8 + 2 * (size_t)T * (M / 2) * 8; }
+int max_q(int NN) {
+    switch (NN) {
+#define X(v) case v: return admm::plan_max_q<v, false>();
+        X(2) X(4) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
+#undef X
+    }
+    return NN;
 }
 int column_KB(int M, int N) {
-    const int L = M / 2;
-    int KB = 16;
-    while (KB > 1 && (size_t)KB * N > 4096) KB >>= 1;
-    if (KB > L) KB = L;
+    int KB = 256 / max_q(N);
+    if (KB > M / 2) KB = M / 2;
+    if (KB > 32) KB = 32;
     return KB;
 }
-size_t column_lds(int N, int KB) { return (size_t)N * 8 + 2 * (size_t)KB * (N + 1) * 8; }
+size_t column_lds(int N, int KB) { return (size_t)N * 16 + (size_t)KB * (N + 1) * 8; }
 
 // ---- profiler -------------------------------------------------------------------------------
 struct Prof {
@@ -155,65 +150,76 @@ struct Launcher {
 };
 
 // ---- template dispatch -----------------------------------------------------------------------
-
-#define ADMM_L_CASES(X) X(2) X(4) X(8) X(16) X(32) X(64) X(128) X(256) X(512)
-#define ADMM_N_CASES(X) X(2) X(4) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
-
 using namespace admm;
 
-int launch_prep(int L, dim3 g, size_t lds, hipStream_t s, const float* y, float* hty, float2* spec0,
-                const float* h, int kh, int kw, const float2* twM, int N, int T) {
-    switch (L) {
-#define X(v)                                                                                  \
-    case v:                                                                                   \
-        hipFuncSetAttribute((const void*)prep_kernel<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        prep_kernel<v><<<g, kThreads, lds, s>>>(y, hty, spec0, h, kh, kw, twM, N, T);          \
-        return 0;
-        ADMM_L_CASES(X)
-#undef X
+template <typename K>
+void set_lds(K kernel, size_t lds) {
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+// (L, T) pairs that line_T() can return
+#define ADMM_LT_CASES(X)                                                                           \
+    X(2, 2) X(2, 4) X(2, 8) X(2, 16) X(4, 2) X(4, 4) X(4, 8) X(4, 16) X(8, 2) X(8, 4) X(8, 8) X(8, 16) \
+    X(16, 2) X(16, 4) X(16, 8) X(16, 16) X(32, 2) X(32, 4) X(32, 8) X(32, 16) X(64, 2) X(64, 4)      \
+    X(64, 8) X(64, 16) X(128, 2) X(128, 4) X(128, 8) X(128, 16) X(256, 2) X(256, 4) X(256, 8)       \
+    X(512, 2) X(512, 4)
+#define ADMM_N_CASES(X) X(2) X(4) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
+
+int launch_line_fwd(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* src, float2* spec,
+                    const float2* twM, int N) {
+#define X(l, t)                                                            \
+    if (L == l && T == t) {                                                \
+        set_lds(line_fwd_kernel<l, t>, lds);                               \
+        line_fwd_kernel<l, t><<<g, kThreads, lds, s>>>(src, spec, twM, N); \
+        return 0;                                                          \
     }
+    ADMM_LT_CASES(X)
+#undef X
     return -1;
 }
 
-int launch_line(int L, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float2* spec0, const float* so,
-                float* sn, const float* hty, const float2* twM, int N, int T, float tau, float rho, int sz) {
-    switch (L) {
-#define X(v)                                                                                  \
-    case v:                                                                                   \
-        hipFuncSetAttribute((const void*)line_kernel<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        line_kernel<v><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, T, tau, rho, sz); \
-        return 0;
-        ADMM_L_CASES(X)
-#undef X
+int launch_line_inv(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec, float* dst,
+                    const float2* twM, int N) {
+#define X(l, t)                                                            \
+    if (L == l && T == t) {                                                \
+        set_lds(line_inv_kernel<l, t>, lds);                               \
+        line_inv_kernel<l, t><<<g, kThreads, lds, s>>>(spec, dst, twM, N); \
+        return 0;                                                          \
     }
+    ADMM_LT_CASES(X)
+#undef X
     return -1;
 }
 
-int launch_final(int L, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float* x, const float2* twM, int N,
-                 int T) {
-    switch (L) {
-#define X(v)                                                                                  \
-    case v:                                                                                   \
-        hipFuncSetAttribute((const void*)final_kernel<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        final_kernel<v><<<g, kThreads, lds, s>>>(spec1, x, twM, N, T);                        \
-        return 0;
-        ADMM_L_CASES(X)
-#undef X
+int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float2* spec0,
+                const float* so, float* sn, const float* hty, const float2* twM, int N, float tau, float rho,
+                int sz) {
+#define X(l, t)                                                                                          \
+    if (L == l && T == t) {                                                                              \
+        set_lds(line_kernel<l, t>, lds);                                                                 \
+        line_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, tau, rho, sz);    \
+        return 0;                                                                                        \
     }
+    ADMM_LT_CASES(X)
+#undef X
     return -1;
 }
 
-int launch_column(int N, dim3 g, size_t lds, hipStream_t s, const float2* spec0, float2* spec1, const float* C,
-                  const float2* twN, int L, int KB) {
-    switch (N) {
-#define X(v)                                                                                  \
-    case v:                                                                                   \
-        hipFuncSetAttribute((const void*)column_kernel<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        column_kernel<v><<<g, kThreads, lds, s>>>(spec0, spec1, C, twN, L, KB);               \
-        return 0;
-        ADMM_N_CASES(X)
-#undef X
+int launch_column(int N, bool cplx, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
+                  const float* C, const float2* G, const float2* twN, int L, int KB, float cs) {
+#define X(v)                                                                                 \
+    if (N == v) {                                                                            \
+        if (cplx) {                                                                          \
+            set_lds(column_kernel<v, true>, lds);                                            \
+            column_kernel<v, true><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs);  \
+        } else {                                                                             \
+            set_lds(column_kernel<v, false>, lds);                                           \
+            column_kernel<v, false><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs); \
+        }                                                                                    \
+        return 0;                                                                            \
     }
+    ADMM_N_CASES(X)
+#undef X
     return -1;
 }
 
@@ -223,10 +229,9 @@ int check_shape(int M, int N, int P, int B, int kh, int kw, int iso) {
         return fail(ADMM_E_INVALID, "PSF size must be both zero (empty PSF) or both positive (kh=%d kw=%d)", kh, kw);
     if (!is_pow2(M) || !is_pow2(N) || M < 4 || M > 1024 || N < 2 || N > 1024)
         return fail(ADMM_E_UNSUPPORTED, "this build supports power-of-two 4<=M<=1024, 2<=N<=1024 (got M=%d N=%d)", M, N);
-    if (kh > M || kw > N || kh * kw > 4096)
-        return fail(ADMM_E_UNSUPPORTED, "PSF %dx%d larger than supported (kh<=M, kw<=N, kh*kw<=4096)", kh, kw);
+    if (kh > M || kw > N)
+        return fail(ADMM_E_UNSUPPORTED, "PSF %dx%d larger than the image (kh<=M, kw<=N required, as pad_constant in ops.jl:25)", kh, kw);
     if (iso) return fail(ADMM_E_UNSUPPORTED, "isotropic (BT) prox is not in this build yet");
-    if (prep_lds(M, prep_T(M, N, kh, kw), kh, kw) > 160 * 1024) return fail(ADMM_E_UNSUPPORTED, "PSF tile exceeds LDS");
     return ADMM_OK;
 }
 
@@ -273,7 +278,8 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
     unsigned char* ws = static_cast<unsigned char*>(workspace);
     float2* twM = reinterpret_cast<float2*>(ws + lay.twM);
     float2* twN = reinterpret_cast<float2*>(ws + lay.twN);
-    float* Cm = reinterpret_cast<float*>(ws + lay.C);
+    float* Ct = reinterpret_cast<float*>(ws + lay.C);
+    float2* Gt = kh > 0 ? reinterpret_cast<float2*>(ws + lay.G) : nullptr;
     float* hty = kh > 0 ? reinterpret_cast<float*>(ws + lay.hty) : const_cast<float*>(y);
     float* sbuf[2] = {reinterpret_cast<float*>(ws + lay.sA), reinterpret_cast<float*>(ws + lay.sB)};
     float2* spec0 = reinterpret_cast<float2*>(ws + lay.spec0);
@@ -286,12 +292,14 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
         const size_t lds = (size_t)(M + N) * 16;
         const int nb = (int)(((size_t)(L + 1) * N + kThreads - 1) / kThreads);
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
-        hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Cm, h, kh, kw, M, N, rho);
+        hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Ct, Gt, h, kh, kw, M,
+                           N, rho);
     });
     if (rc) return rc;
 
-    const int Tp = prep_T(M, N, kh, kw), Tl = line_T(M, N), Tf = line_T(M, N);
+    const int T = line_T(M, N);
     const int KB = column_KB(M, N);
+    const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
     const int kMaxY = 65535;
     for (size_t p0 = 0; p0 < planes; p0 += kMaxY) {
         const int np = (int)((planes - p0) < (size_t)kMaxY ? (planes - p0) : (size_t)kMaxY);
@@ -302,27 +310,34 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
         float* sa = sbuf[0] + p0 * 2 * MN;
         float* sb = sbuf[1] + p0 * 2 * MN;
         float* xp = x_out + p0 * MN;
-        rc = ln.run(ADMM_K_PREP, [&] {
-            launch_prep(L, dim3(N / Tp, np), prep_lds(M, Tp, kh, kw), s, yp, kh > 0 ? htyp : nullptr, sp0, h, kh, kw,
-                        twM, N, Tp);
-        });
+        const dim3 gl(N / T, np), gc(L / KB, np);
+        // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
+        rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, yp, sp0, twM, N); });
         if (rc) return rc;
+        const float2* first = sp0;
+        float cs1 = 1.0f;
+        if (kh > 0) {
+            rc = ln.run(ADMM_K_PREP, [&] { launch_column(N, true, gc, clds, s, sp0, sp1, Ct, Gt, twN, L, KB, 1.0f); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_PREP, [&] { launch_line_inv(L, T, gl, flds, s, sp1, htyp, twM, N); });
+            if (rc) return rc;
+            first = sp1;          // = F_dim1(H^T y) / M
+            cs1 = (float)M;
+        }
         for (int it = 1; it <= maxit; ++it) {
             rc = ln.run(ADMM_K_COLUMN, [&] {
-                launch_column(N, dim3(L / KB, np), column_lds(N, KB), s, sp0, sp1, Cm, twN, L, KB);
+                launch_column(N, false, gc, clds, s, it == 1 ? first : sp0, sp1, Ct, Gt, twN, L, KB,
+                              it == 1 ? cs1 : 1.0f);
             });
             if (rc) return rc;
             if (it < maxit) {
                 float* so = (it & 1) ? sb : sa;   // iteration 1 reads nothing (s_zero)
                 float* sn = (it & 1) ? sa : sb;
                 rc = ln.run(ADMM_K_LINE, [&] {
-                    launch_line(L, dim3(N / Tl, np), line_lds(M, Tl), s, sp1, sp0, so, sn, htyp, twM, N, Tl, tau, rho,
-                                it == 1 ? 1 : 0);
+                    launch_line(L, T, gl, llds, s, sp1, sp0, so, sn, htyp, twM, N, tau, rho, it == 1 ? 1 : 0);
                 });
             } else {
-                rc = ln.run(ADMM_K_FINAL, [&] {
-                    launch_final(L, dim3(N / Tf, np), final_lds(M, Tf), s, sp1, xp, twM, N, Tf);
-                });
+                rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, sp1, xp, twM, N); });
             }
             if (rc) return rc;
         }

@@ -1,41 +1,48 @@
 // admm_kernels.hip -- MI355X (gfx950) kernels for the ADMM TV-deconvolution solve.
 //
-// Replaces the per-iteration CUFFT/cuDNN/broadcast chain of tvd_fft_gpu
+// Replaces the per-iteration CUFFT / cuDNN / broadcast chain of tvd_fft_gpu
 // (/root/reference/src/ops/ops.jl:99-178) with two fused passes per iteration:
 //
-//   COLUMN pass  (ops.jl:168, the dim2 half of rfft/irfft and the C .* scale):
-//       spec0[plane][j][k]  --FFT_j--> xC[k][kj] --IFFT_j-->  spec1[plane][j][k]
-//   LINE pass    (ops.jl:168-173 + the dim1 half of the transforms):
+//   COLUMN pass  (ops.jl:168: the dim2 half of rfft/irfft and the C .* scale)
+//       spec[plane][j][k]  --FFT_j--> x C[k][kj] --IFFT_j-->  spec1[plane][j][k]      (in place OK)
+//   LINE pass    (ops.jl:168-173 + the dim1 half of the transforms)
 //       spec1 --irFFT_i--> x --D--> s = Dx + u --prox--> w = z-u --D^T--> v = H^T y + rho D^T w
-//       --rFFT_i--> spec0,     s written back (ping-pong) as the only per-pixel ADMM state.
+//       --rFFT_i--> spec0, and s written back (ping-pong) as the only per-pixel ADMM state.
 //
-// State compression: with s_k = Dx_k + u_{k-1} the reference's z_k = ST(s_k) and
-// u_k = s_k - z_k = clip(s_k, -tau, tau), so z_k - u_k and u_k are functions of s_k alone; one
-// 2-channel fp32 tensor replaces the reference's Dx, z, u (ops.jl:128-131).
+// State compression: with s_k = Dx_k + u_{k-1}, the reference's z_k = ST(s_k) and
+// u_k = s_k - z_k = clip(s_k, -tau, tau) are functions of s_k alone, so one 2-channel fp32 tensor
+// replaces the reference's Dx, z and u (ops.jl:128-131).
 //
-// Half-spectrum packing: a line of M reals has M/2+1 bins, of which bin 0 and bin M/2 are real.
-// They share slot 0 as (X[0], X[M/2]), so each line's spectrum is exactly M/2 complex
-// (1 KiB for M = 256) and the column pass handles slot 0 with the (C[0]+C[M/2])/2,
-// (C[0]-C[M/2])/2 mirror form (both rows of C are even in kj).
+// Half-spectrum packing: a line of M reals has M/2+1 bins; bins 0 and M/2 are real and share slot 0
+// as (X[0], X[M/2]), so a line's spectrum is exactly M/2 complex (1 KiB at M = 256).  Rows k = 0 and
+// k = M/2 of any multiplier used here are Hermitian in kj, so the column pass applies slot 0 as
+//   R[kj] = (m0+mL)/2 Z[kj] + (m0-mL)/2 conj(Z[-kj]).
 //
-// Real <-> half-length complex: z[m] = x[2m] + i x[2m+1]; Z = FFT_{M/2}(z);
+// Real <-> half-length complex: z[n] = x[2n] + i x[2n+1]; Z = FFT_{M/2}(z);
 //   X[k] = E[k] + W_M^k O[k], E = (Z[k] + conj Z[L-k])/2, O = (Z[k] - conj Z[L-k])/(2i).
-// All transforms are unnormalised; 1/(M N) is folded into C.
+// All transforms are unnormalised; 1/(M N) is folded into the multiplier tables.
+//
+// H^T y (ops.jl:71-81) is evaluated ONCE (the reference re-evaluates it every iteration and gets the
+// same array) and spectrally: H^T y = F^-1[ conj(Sigma_c) F y ] with Sigma_c the spectrum of the
+// centred PSF -- the same line/column kernels with a complex multiplier.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "fft_lds.hpp"
+#include "fft_reg.hpp"
 
 namespace admm {
 
 constexpr int kThreads = 256;
 
 // ----------------------------------------------------------------------------------------------
-// setup: twiddle tables (double-built) and the C spectrum (ops.jl:22-37)
+// setup: twiddle tables and multiplier tables, built in fp64 (ops.jl:22-37)
+//   Ct[kj][k] = 1/(MN) / (|Sigma|^2 + rho(|Lx|^2 + |Ly|^2))     k = 0..M/2  (transposed: k fastest)
+//   Gt[kj][k] = 1/(MN) * conj(Sigma_centred)                      (only with a PSF)
 // ----------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ twM, float2* __restrict__ twN,
-                                                         float* __restrict__ Cmat, const float* __restrict__ h,
-                                                         int kh, int kw, int M, int N, float rho) {
+                                                         float* __restrict__ Ct, float2* __restrict__ Gt,
+                                                         const float* __restrict__ h, int kh, int kw, int M,
+                                                         int N, float rho) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     double2* tM = reinterpret_cast<double2*>(smem_raw);  // exp(-2 pi i t / M)
     double2* tN = tM + M;                                // exp(-2 pi i t / N)
@@ -50,18 +57,18 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
         tN[t] = make_double2(c, s);
     }
     __syncthreads();
-    const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int gsz = gridDim.x * blockDim.x;
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < M; t += blockDim.x) twM[t] = make_float2((float)tM[t].x, (float)tM[t].y);
         for (int t = threadIdx.x; t < N; t += blockDim.x) twN[t] = make_float2((float)tN[t].x, (float)tN[t].y);
     }
     const int L = M / 2;
-    const int nbins = (L + 1) * N;
+    const int H = L + 1;
+    const int nbins = H * N;
     const double inv_mn = 1.0 / ((double)M * (double)N);
-    for (int q = gtid; q < nbins; q += gsz) {
-        const int k = q / N;   // dim1 frequency 0..L
-        const int kj = q - k * N;
+    const int padd = (kh - 1) / 2, padr = (kw - 1) / 2;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nbins; q += gridDim.x * blockDim.x) {
+        const int kj = q / H;   // dim2 frequency
+        const int k = q - kj * H;  // dim1 frequency 0..L
         double s2 = 1.0;
         if (kh > 0) {
             double re = 0.0, im = 0.0;
@@ -78,72 +85,63 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
                 im += gr * eb.y + gi * eb.x;
             }
             s2 = re * re + im * im;
+            // centred spectrum: Sigma_c = Sigma * exp(+2 pi i (padd k/M + padr kj/N)); store conj / (MN)
+            const double2 pa = tM[(padd * k) & (M - 1)];
+            const double2 pb = tN[(padr * kj) & (N - 1)];
+            const double pr = pa.x * pb.x - pa.y * pb.y, pi = pa.x * pb.y + pa.y * pb.x;  // exp(-i phi)
+            // Sigma_c = Sigma * conj(p);  conj(Sigma_c) = conj(Sigma) * p
+            const double cr = re * pr + im * pi;
+            const double ci = re * pi - im * pr;
+            Gt[q] = make_float2((float)(cr * inv_mn), (float)(ci * inv_mn));
         }
         const double sx = sinpi((double)kj / (double)N), sy = sinpi((double)k / (double)M);
         const double lap = 4.0 * sx * sx + 4.0 * sy * sy;   // |Lx|^2 + |Ly|^2 (ops.jl:35-36)
-        Cmat[q] = (float)(inv_mn / (s2 + (double)rho * lap));
+        Ct[q] = (float)(inv_mn / (s2 + (double)rho * lap));
     }
 }
 
 // ----------------------------------------------------------------------------------------------
-// helpers for the line kernels
+// line helpers
 // ----------------------------------------------------------------------------------------------
-// half-spectrum (packed, L slots) -> half-length complex Z, ready for the inverse L-point FFT
+// Z[n] of the inverse half-length transform, from the packed half spectrum X of one line (LDS)
 template <int L>
-__device__ __forceinline__ void unpack_inverse(const float2* __restrict__ X, float2* __restrict__ Z, int nlines,
-                                               const float2* __restrict__ tw) {
+__device__ __forceinline__ float2 unpack_z(const float2* __restrict__ Xl, int n, const float2* __restrict__ tw) {
+    if (n == 0) {
+        const float2 p = Xl[0];  // (X[0], X[M/2]), both real
+        return make_float2(p.x + p.y, p.x - p.y);
+    }
+    const float2 xk = Xl[n];
+    const float2 xm = cconj(Xl[L - n]);
+    const float2 e = cadd(xk, xm);
+    const float2 o = cmul(csub(xk, xm), cconj(tw[n]));  // * W_M^{-n}
+    return make_float2(e.x - o.y, e.y + o.x);            // E + i O
+}
+
+// packed half-spectrum bin k of a real line from its half-length transform Z (LDS)
+template <int L>
+__device__ __forceinline__ float2 pack_x(const float2* __restrict__ Zl, int k, const float2* __restrict__ tw) {
+    if (k == 0) {
+        const float2 z0 = Zl[0];
+        return make_float2(z0.x + z0.y, z0.x - z0.y);
+    }
+    const float2 zk = Zl[k];
+    const float2 zm = cconj(Zl[L - k]);
+    const float2 e = cscale(cadd(zk, zm), 0.5f);
+    const float2 d = csub(zk, zm);
+    const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);  // d / (2i)
+    return cadd(e, cmul(tw[k], o));
+}
+
+template <int L>
+__device__ __forceinline__ void pack_store(const float2* __restrict__ Z, float2* __restrict__ out_plane, int j0,
+                                           int nlines, int N, const float2* __restrict__ tw) {
     for (int idx = threadIdx.x; idx < nlines * L; idx += blockDim.x) {
         const int t = idx / L;
         const int k = idx - t * L;
-        const float2* Xl = X + t * L;
-        float2 z;
-        if (k == 0) {
-            const float2 p = Xl[0];  // (X[0], X[M/2]), both real
-            z = make_float2(p.x + p.y, p.x - p.y);
-        } else {
-            const float2 xk = Xl[k];
-            const float2 xm = cconj(Xl[L - k]);
-            const float2 e = cadd(xk, xm);
-            const float2 o = cmul(csub(xk, xm), cconj(tw[k]));  // * W_M^{-k}
-            z = make_float2(e.x - o.y, e.y + o.x);               // E + i O
-        }
-        Z[idx] = z;
+        out_plane[(size_t)((j0 + t) & (N - 1)) * L + k] = pack_x<L>(Z + t * L, k, tw);
     }
 }
 
-// half-length complex spectrum Z -> packed half-spectrum of the real line; writes to global
-template <int L>
-__device__ __forceinline__ void pack_forward_store(const float2* __restrict__ Z, float2* __restrict__ out_plane,
-                                                   int j0, int nlines, int N, const float2* __restrict__ tw) {
-    for (int idx = threadIdx.x; idx < nlines * L; idx += blockDim.x) {
-        const int t = idx / L;
-        const int k = idx - t * L;
-        const float2* Zl = Z + t * L;
-        float2 X;
-        if (k == 0) {
-            const float2 z0 = Zl[0];
-            X = make_float2(z0.x + z0.y, z0.x - z0.y);
-        } else {
-            const float2 zk = Zl[k];
-            const float2 zm = cconj(Zl[L - k]);
-            const float2 e = cscale(cadd(zk, zm), 0.5f);
-            const float2 d = csub(zk, zm);
-            const float2 o = make_float2(0.5f * d.y, -0.5f * d.x);  // d / (2i)
-            X = cadd(e, cmul(tw[k], o));
-        }
-        const int g = (j0 + t) & (N - 1);
-        out_plane[(size_t)g * L + k] = X;
-    }
-}
-
-__device__ __forceinline__ float clipf(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
-// w = z - u for z = ST(s,tau), u = s - z   (ops.jl:9, :171-173)
-__device__ __forceinline__ float prox_w(float s, float tau) {
-    const float a = fabsf(s);
-    return a > tau ? s - copysignf(2.0f * tau, s) : -s;
-}
-
-// load `nlines` packed spectrum lines (j0 + t) mod N into LDS
 template <int L>
 __device__ __forceinline__ void load_lines(const float2* __restrict__ plane, float2* __restrict__ dst, int j0,
                                            int nlines, int N) {
@@ -153,234 +151,395 @@ __device__ __forceinline__ void load_lines(const float2* __restrict__ plane, flo
     for (int idx = threadIdx.x; idx < nlines * L2; idx += blockDim.x) {
         const int t = idx / L2;
         const int q = idx - t * L2;
-        const int g = (j0 + t) & (N - 1);
-        d4[idx] = src4[(size_t)g * L2 + q];
+        d4[idx] = src4[(size_t)((j0 + t) & (N - 1)) * L2 + q];
     }
 }
 
+__device__ __forceinline__ float clipf(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
+// w = z - u for z = ST(s, tau), u = s - z  (ops.jl:9, :171-173)
+__device__ __forceinline__ float prox_w(float s, float tau) {
+    return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s;
+}
+
 // ----------------------------------------------------------------------------------------------
-// PREP: H^T y (ops.jl:71-81, computed ONCE; the reference recomputes it every iteration) and the
-// first iteration's v = H^T y  (z = u = 0)  ->  rFFT along dim1  ->  spec0
+// LINE_FWD: rFFT along dim1 of T real lines of a plane (y or any real field) -> packed spectrum
 // ----------------------------------------------------------------------------------------------
-template <int L>
-__global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict__ y, float* __restrict__ hty,
-                                                        float2* __restrict__ spec0, const float* __restrict__ h,
-                                                        int kh, int kw, const float2* __restrict__ twM, int N,
-                                                        int T) {
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void line_fwd_kernel(const float* __restrict__ src, float2* __restrict__ spec,
+                                                            const float2* __restrict__ twM, int N) {
+    constexpr int M = 2 * L;
+    constexpr int P = Plan<L>::P;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float2* X = tw + M;
+    float2* Bf = X + T * L;
+    const int plane = blockIdx.y;
+    const int j0 = blockIdx.x * T;
+    for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
+    __syncthreads();
+    const float2* sp = reinterpret_cast<const float2*>(src + (size_t)plane * N * M);
+    auto gload = [&](int f, int n) { return sp[(size_t)(j0 + f) * L + n]; };
+    float2* Z = (P == 2) ? Bf : X;
+    fft_plan<L, true, false, 2>(T, tw, X, Bf, L, gload, LdsIO{Z, L});
+    __syncthreads();
+    pack_store<L>(Z, spec + (size_t)plane * N * L, j0, T, N, tw);
+}
+
+// ----------------------------------------------------------------------------------------------
+// LINE_INV: irFFT along dim1 of T lines -> real lines (final x, or H^T y during setup)
+// ----------------------------------------------------------------------------------------------
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __restrict__ spec, float* __restrict__ dst,
+                                                            const float2* __restrict__ twM, int N) {
     constexpr int M = 2 * L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
-    float2* A = tw + M;
-    float2* Bb = A + T * L;
-    float* hs = reinterpret_cast<float*>(Bb + T * L);
-    float* tile = hs + ((kh * kw + 3) & ~3);
+    float2* X = tw + M;
+    float2* Bf = X + T * L;
     const int plane = blockIdx.y;
     const int j0 = blockIdx.x * T;
-    const float* yp = y + (size_t)plane * N * M;
     for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
-    float* a_f = reinterpret_cast<float*>(A);
-    if (kh > 0) {
-        const int padd = (kh - 1) / 2, padr = (kw - 1) / 2;
-        for (int t = threadIdx.x; t < kh * kw; t += blockDim.x) hs[t] = h[t];
-        const int rows = T + kw - 1;
-        constexpr int M4 = M / 4;
-        for (int idx = threadIdx.x; idx < rows * M4; idx += blockDim.x) {
-            const int r = idx / M4;
-            const int q = idx - r * M4;
-            const int g = (j0 - padr + r) & (N - 1);
-            reinterpret_cast<float4*>(tile)[idx] = reinterpret_cast<const float4*>(yp + (size_t)g * M)[q];
-        }
-        __syncthreads();
-        float* hp = hty + (size_t)plane * N * M;
-        for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-            const int t = idx / M;
-            const int i = idx - t * M;
-            float acc = 0.0f;
-            for (int b = 0; b < kw; ++b) {
-                const float* row = tile + (t + b) * M;
-                const float* hb = hs + b * kh;
-                for (int a = 0; a < kh; ++a) acc = fmaf(hb[a], row[(i + a - padd) & (M - 1)], acc);
-            }
-            a_f[idx] = acc;
-            hp[(size_t)((j0 + t) & (N - 1)) * M + i] = acc;
-        }
-    } else {
-        constexpr int M4 = M / 4;
-        for (int idx = threadIdx.x; idx < T * M4; idx += blockDim.x) {
-            const int t = idx / M4;
-            const int q = idx - t * M4;
-            const int g = (j0 + t) & (N - 1);
-            reinterpret_cast<float4*>(a_f)[idx] = reinterpret_cast<const float4*>(yp + (size_t)g * M)[q];
-        }
-    }
+    load_lines<L>(spec + (size_t)plane * N * L, X, j0, T, N);
     __syncthreads();
-    float2* R = fft_lds<L, false, 2>(A, Bb, T, L, tw);
-    pack_forward_store<L>(R, spec0 + (size_t)plane * N * L, j0, T, N, tw);
+    float2* dp = reinterpret_cast<float2*>(dst + (size_t)plane * N * M);
+    auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
+    auto gstore = [&](int f, int n, float2 v) { dp[(size_t)(j0 + f) * L + n] = v; };
+    fft_plan<L, false, true, 2>(T, tw, Bf, X, L, uload, gstore);
 }
 
 // ----------------------------------------------------------------------------------------------
-// COLUMN pass: for KB consecutive slots of one plane, FFT along dim2 (N points), multiply by C,
-// inverse FFT along dim2.  The slot-0 pair (X[0], X[M/2]) uses the even-symmetric mirror form.
+// COLUMN pass: KB consecutive slots of one plane; FFT along dim2 (NN points), multiply, inverse.
+// Forward plan, then the reversed plan for the inverse, so the forward's last pass and the inverse's
+// first pass touch the same points in the same thread: they run back to back in registers with the
+// multiply between (one LDS round trip saved).  One LDS buffer, in-place passes (read, barrier,
+// write); requires KB * NN / R <= blockDim for every radix R of the plan (host guarantees).
+//   CPLX = false: real multiplier Ct (the ADMM x-update), scaled by cs
+//   CPLX = true : complex multiplier Gt (H^T y setup)
 // ----------------------------------------------------------------------------------------------
-template <int NN>
-__global__ __launch_bounds__(kThreads) void column_kernel(const float2* __restrict__ spec0, float2* __restrict__ spec1,
-                                                          const float* __restrict__ Cmat,
-                                                          const float2* __restrict__ twN, int L, int KB) {
-    constexpr int FS = NN + 1;  // padded per-transform stride (transposed staging)
+template <int NN, bool CPLX>
+__global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, float2* dst,
+                                                          const float* __restrict__ Ct,
+                                                          const float2* __restrict__ Gt,
+                                                          const float2* __restrict__ twN, int L, int KB, float cs) {
+    constexpr int FS = NN + 1;  // per-transform LDS stride (odd: conflict-free slot-major stores)
+    constexpr int P = Plan<NN>::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
-    float2* A = tw + NN;
-    float2* Bb = A + KB * FS;
+    float2* S0 = tw + NN;        // slot-0 spectrum for the mirror term
+    float2* buf = S0 + NN;
     const int plane = blockIdx.y;
     const int k0 = blockIdx.x * KB;
-    const float2* src = spec0 + (size_t)plane * NN * L + k0;
-    float2* dst = spec1 + (size_t)plane * NN * L + k0;
+    const int H = L + 1;
+    const float2* gsrc = src + (size_t)plane * NN * L + k0;
+    float2* gdst = dst + (size_t)plane * NN * L + k0;
     for (int t = threadIdx.x; t < NN; t += blockDim.x) tw[t] = twN[t];
-    for (int idx = threadIdx.x; idx < KB * NN; idx += blockDim.x) {
-        const int j = idx / KB;
-        const int kk = idx - j * KB;
-        A[kk * FS + j] = src[(size_t)j * L + kk];
-    }
     __syncthreads();
-    float2* R = fft_lds<NN, false, 1>(A, Bb, KB, FS, tw);
-    float2* O = (R == A) ? Bb : A;
-    for (int idx = threadIdx.x; idx < KB * NN; idx += blockDim.x) {
-        const int kk = idx / NN;
-        const int kj = idx - kk * NN;
-        const int k = k0 + kk;
-        const float2 z = R[kk * FS + kj];
-        float2 o;
-        if (k == 0) {
-            const float c0 = Cmat[kj], cL = Cmat[(size_t)L * NN + kj];
-            const float2 zm = cconj(R[kk * FS + ((NN - kj) & (NN - 1))]);
-            o = cadd(cscale(z, 0.5f * (c0 + cL)), cscale(zm, 0.5f * (c0 - cL)));
-        } else {
-            o = cscale(z, Cmat[(size_t)k * NN + kj]);
+    const int tid = threadIdx.x;
+    // ---- forward pass 0: global -> regs -> LDS   (thread = (j, f), slot f fastest) ----
+    {
+        constexpr int R = plan_radix<NN, 0, false>();
+        constexpr int Q = NN / R;
+        if (tid < KB * Q) {
+            const int f = tid % KB, j = tid / KB;
+            float2 v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = gsrc[(size_t)(j + r * Q) * L + f];
+            if constexpr (P == 1) {
+                // single-pass plan: handled below in the fused step (no LDS staging needed)
+            }
+            fly_core<NN, R, 0, false, 1>(v, j, tw);
+            const int o = out_base<NN, R, 0>(j);
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[f * FS + o + r] = v[r];
         }
-        O[kk * FS + kj] = o;
     }
     __syncthreads();
-    float2* R2 = fft_lds<NN, true, 1>(O, R, KB, FS, tw);
-    for (int idx = threadIdx.x; idx < KB * NN; idx += blockDim.x) {
-        const int j = idx / KB;
-        const int kk = idx - j * KB;
-        dst[(size_t)j * L + kk] = R2[kk * FS + j];
+    if constexpr (P == 3) {   // forward middle pass, in place
+        constexpr int R = plan_radix<NN, 1, false>();
+        constexpr int LG = plan_lgns<NN, 1, false>();
+        constexpr int Q = NN / R;
+        float2 v[R];
+        const int f = tid % KB, j = tid / KB;
+        const bool act = tid < KB * Q;
+        if (act) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
+        }
+        __syncthreads();
+        if (act) {
+            fly_core<NN, R, LG, false, 1>(v, j, tw);
+            const int o = out_base<NN, R, LG>(j);
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[f * FS + o + r * (1 << LG)] = v[r];
+        }
+        __syncthreads();
+    }
+    // ---- fused: forward last pass -> multiply -> inverse first pass ----
+    {
+        constexpr int PL = P - 1;
+        constexpr int R = plan_radix<NN, PL, false>();
+        constexpr int LG = plan_lgns<NN, PL, false>();
+        constexpr int Q = NN / R;   // == Ns of the last pass: outputs at j + r*Q
+        float2 v[R];
+        const int f = tid % KB, j = tid / KB;
+        const bool act = tid < KB * Q;
+        const bool mirror = (k0 == 0);  // block-uniform
+        if (act) {
+            if constexpr (P > 1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
+                fly_core<NN, R, LG, false, 1>(v, j, tw);
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
+            }
+            if (mirror && f == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) S0[j + r * Q] = v[r];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            const int s = k0 + f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int kj = j + r * Q;
+                if (mirror && f == 0) {
+                    const float2 zm = cconj(S0[(NN - kj) & (NN - 1)]);
+                    if constexpr (CPLX) {
+                        const float2 m0 = Gt[(size_t)kj * H], mL = Gt[(size_t)kj * H + L];
+                        const float2 a = cscale(cadd(m0, mL), 0.5f), b = cscale(csub(m0, mL), 0.5f);
+                        v[r] = cadd(cmul(a, v[r]), cmul(b, zm));
+                    } else {
+                        const float c0 = Ct[(size_t)kj * H], cL = Ct[(size_t)kj * H + L];
+                        v[r] = cadd(cscale(v[r], 0.5f * cs * (c0 + cL)), cscale(zm, 0.5f * cs * (c0 - cL)));
+                    }
+                } else {
+                    if constexpr (CPLX) {
+                        v[r] = cmul(v[r], Gt[(size_t)kj * H + s]);
+                    } else {
+                        v[r] = cscale(v[r], cs * Ct[(size_t)kj * H + s]);
+                    }
+                }
+            }
+            // inverse first pass (reversed plan: radix R, Ns = 1) reads exactly j + r*Q
+            dft<R, true>(v);
+            if constexpr (P == 1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) gdst[(size_t)(j * R + r) * L + f] = v[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) buf[f * FS + j * R + r] = v[r];
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (P == 3) {   // inverse middle pass (reversed plan pass 1), in place
+        constexpr int R = plan_radix<NN, 1, true>();
+        constexpr int LG = plan_lgns<NN, 1, true>();
+        constexpr int Q = NN / R;
+        float2 v[R];
+        const int f = tid % KB, j = tid / KB;
+        const bool act = tid < KB * Q;
+        if (act) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
+        }
+        __syncthreads();
+        if (act) {
+            fly_core<NN, R, LG, true, 1>(v, j, tw);
+            const int o = out_base<NN, R, LG>(j);
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[f * FS + o + r * (1 << LG)] = v[r];
+        }
+        __syncthreads();
+    }
+    if constexpr (P > 1) {    // inverse last pass: LDS -> regs -> global
+        constexpr int PL = P - 1;
+        constexpr int R = plan_radix<NN, PL, true>();
+        constexpr int LG = plan_lgns<NN, PL, true>();
+        constexpr int Q = NN / R;
+        if (tid < KB * Q) {
+            const int f = tid % KB, j = tid / KB;
+            float2 v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
+            fly_core<NN, R, LG, true, 1>(v, j, tw);
+            const int o = out_base<NN, R, LG>(j);
+#pragma unroll
+            for (int r = 0; r < R; ++r) gdst[(size_t)(o + r * (1 << LG)) * L + f] = v[r];
+        }
     }
 }
 
 // ----------------------------------------------------------------------------------------------
 // LINE pass (iterations 1..K-1): T output lines + 1 halo line on each side.
 // ----------------------------------------------------------------------------------------------
-template <int L>
+template <int L, int T>
 __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict__ spec1, float2* __restrict__ spec0,
                                                         const float* __restrict__ s_old, float* __restrict__ s_new,
                                                         const float* __restrict__ hty,
-                                                        const float2* __restrict__ twM, int N, int T, float tau,
-                                                        float rho, int s_zero) {
+                                                        const float2* __restrict__ twM, int N, float tau, float rho,
+                                                        int s_zero) {
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
-    const int TH = T + 2;
+    constexpr int TH = T + 2;
+    constexpr int P = Plan<L>::P;
+    constexpr int NE = (T + 1) * M4;                       // float4 items of the elementwise step
+    constexpr int NIT = (NE + kThreads - 1) / kThreads;
+    constexpr int RF = plan_radix<L, 0, true>();           // forward (reversed plan) first radix
+    constexpr int QF = L / RF;
+    constexpr int NITF = (T * QF + kThreads - 1) / kThreads;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
-    float2* A = tw + M;
-    float2* Bb = A + TH * L;
-    float* W1 = reinterpret_cast<float*>(Bb + TH * L);  // T lines of M
+    float2* X = tw + M;           // TH lines
+    float2* Bf = X + TH * L;      // TH lines
+    float2* Cf = Bf + TH * L;     // TH lines (w1; 3rd ping-pong buffer for 3-pass plans)
     const int plane = blockIdx.y;
     const int j0 = blockIdx.x * T;
     const size_t MN = (size_t)M * N;
-    for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
-    load_lines<L>(spec1 + (size_t)plane * N * L, A, j0 - 1, TH, N);
-    __syncthreads();
-    unpack_inverse<L>(A, Bb, TH, tw);
-    __syncthreads();
-    float2* Xc = fft_lds<L, true, 2>(Bb, A, TH, L, tw);  // x lines j0-1 .. j0+T
-    float* X = reinterpret_cast<float*>(Xc);
-    float* W0 = reinterpret_cast<float*>(Xc == A ? Bb : A);  // T+1 lines
+    const int tid = threadIdx.x;
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
-    // s = Dx + u_old ; w = z - u   (ops.jl:169-173)
-    for (int idx = threadIdx.x; idx < (T + 1) * M4; idx += blockDim.x) {
+    const float* hp = hty + (size_t)plane * MN;
+
+    // ---- issue every global load of the block up front ----
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
+    float4 pre0[NIT], pre1[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int idx = tid + it * kThreads;
         const int t = idx / M4;
         const int i = (idx - t * M4) * 4;
-        const int g = (j0 + t) & (N - 1);
-        const float4 xc = *reinterpret_cast<const float4*>(X + (t + 1) * M + i);
-        const float4 xp = *reinterpret_cast<const float4*>(X + t * M + i);
-        float4 so0 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!s_zero) so0 = *reinterpret_cast<const float4*>(so + (size_t)g * M + i);
-        float4 s0;
-        s0.x = (xc.x - xp.x) + clipf(so0.x, tau);
-        s0.y = (xc.y - xp.y) + clipf(so0.y, tau);
-        s0.z = (xc.z - xp.z) + clipf(so0.z, tau);
-        s0.w = (xc.w - xp.w) + clipf(so0.w, tau);
-        float4 w0 = make_float4(prox_w(s0.x, tau), prox_w(s0.y, tau), prox_w(s0.z, tau), prox_w(s0.w, tau));
-        *reinterpret_cast<float4*>(W0 + t * M + i) = w0;
-        if (t < T) {
-            const float xl = X[(t + 1) * M + ((i - 1) & (M - 1))];
-            float4 so1 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (!s_zero) so1 = *reinterpret_cast<const float4*>(so + MN + (size_t)g * M + i);
-            float4 s1;
-            s1.x = (xc.x - xl) + clipf(so1.x, tau);
-            s1.y = (xc.y - xc.x) + clipf(so1.y, tau);
-            s1.z = (xc.z - xc.y) + clipf(so1.z, tau);
-            s1.w = (xc.w - xc.z) + clipf(so1.w, tau);
-            float4 w1 = make_float4(prox_w(s1.x, tau), prox_w(s1.y, tau), prox_w(s1.z, tau), prox_w(s1.w, tau));
-            *reinterpret_cast<float4*>(W1 + t * M + i) = w1;
-            *reinterpret_cast<float4*>(sn + (size_t)g * M + i) = s0;
-            *reinterpret_cast<float4*>(sn + MN + (size_t)g * M + i) = s1;
+        const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+        pre0[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pre1[it] = pre0[it];
+        if (!s_zero && idx < NE) {
+            pre0[it] = *reinterpret_cast<const float4*>(so + off);
+            if (t < T) pre1[it] = *reinterpret_cast<const float4*>(so + MN + off);
+        }
+    }
+    float2 preh[NITF][RF];
+#pragma unroll
+    for (int it = 0; it < NITF; ++it) {
+        const int idx = tid + it * kThreads;
+        const int f = idx / QF, j = idx - f * QF;
+        if (idx < T * QF) {
+            const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
+#pragma unroll
+            for (int r = 0; r < RF; ++r) preh[it][r] = hl[j + r * QF];
         }
     }
     __syncthreads();
-    // v = H^T y + rho * D^T w   (ops.jl:168)
-    const float* hp = hty + (size_t)plane * MN;
-    for (int idx = threadIdx.x; idx < T * M4; idx += blockDim.x) {
-        const int t = idx / M4;
-        const int i = (idx - t * M4) * 4;
-        const int g = (j0 + t) & (N - 1);
-        const float4 a0 = *reinterpret_cast<const float4*>(W0 + t * M + i);
-        const float4 a1 = *reinterpret_cast<const float4*>(W0 + (t + 1) * M + i);
-        const float4 b0 = *reinterpret_cast<const float4*>(W1 + t * M + i);
-        const float bn = W1[t * M + ((i + 4) & (M - 1))];
-        const float4 hv = *reinterpret_cast<const float4*>(hp + (size_t)g * M + i);
-        float4 v;
-        v.x = fmaf(rho, (a0.x - a1.x) + (b0.x - b0.y), hv.x);
-        v.y = fmaf(rho, (a0.y - a1.y) + (b0.y - b0.z), hv.y);
-        v.z = fmaf(rho, (a0.z - a1.z) + (b0.z - b0.w), hv.z);
-        v.w = fmaf(rho, (a0.w - a1.w) + (b0.w - bn), hv.w);
-        *reinterpret_cast<float4*>(X + t * M + i) = v;
-    }
-    __syncthreads();
-    float2* Vin = reinterpret_cast<float2*>(X);
-    float2* scratch = reinterpret_cast<float2*>(W0);
-    float2* R = fft_lds<L, false, 2>(Vin, scratch, T, L, tw);
-    pack_forward_store<L>(R, spec0 + (size_t)plane * N * L, j0, T, N, tw);
-}
 
-// ----------------------------------------------------------------------------------------------
-// FINAL: last iteration's irFFT along dim1 -> x (ops.jl:168, :175)
-// ----------------------------------------------------------------------------------------------
-template <int L>
-__global__ __launch_bounds__(kThreads) void final_kernel(const float2* __restrict__ spec1, float* __restrict__ x,
-                                                         const float2* __restrict__ twM, int N, int T) {
-    constexpr int M = 2 * L;
-    constexpr int M4 = M / 4;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    float2* tw = reinterpret_cast<float2*>(smem_raw);
-    float2* A = tw + M;
-    float2* Bb = A + T * L;
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
-    for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
-    load_lines<L>(spec1 + (size_t)plane * N * L, A, j0, T, N);
-    __syncthreads();
-    unpack_inverse<L>(A, Bb, T, tw);
-    __syncthreads();
-    float* X = reinterpret_cast<float*>(fft_lds<L, true, 2>(Bb, A, T, L, tw));
-    float* xp = x + (size_t)plane * N * M;
-    for (int idx = threadIdx.x; idx < T * M4; idx += blockDim.x) {
-        const int t = idx / M4;
-        const int q = idx - t * M4;
-        reinterpret_cast<float4*>(xp + (size_t)(j0 + t) * M)[q] = reinterpret_cast<const float4*>(X + t * M)[q];
+    // ---- irFFT along dim1 of TH lines: x (float view of the result buffer) ----
+    auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
+    float2* Xr;
+    if constexpr (P == 1) {
+        Xr = Bf;
+        fpass<L, L, 0, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+    } else if constexpr (P == 2) {
+        Xr = X;  // pass 0: X -> Bf ; pass 1: Bf -> X
+        fft_plan<L, false, true, 2>(TH, tw, Bf, Cf, L, uload, LdsIO{X, L});
+    } else {
+        Xr = Bf;  // X -> Bf -> Cf -> Bf
+        plan_pass<L, 0, false, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+        __syncthreads();
+        plan_pass<L, 1, false, true, 2>(TH, tw, LdsIO{Bf, L}, LdsIO{Cf, L});
+        __syncthreads();
+        plan_pass<L, 2, false, true, 2>(TH, tw, LdsIO{Cf, L}, LdsIO{Bf, L});
     }
+    __syncthreads();
+    const float* x = reinterpret_cast<const float*>(Xr);
+    float* W0 = reinterpret_cast<float*>(Xr == X ? Bf : X);   // T+1 lines
+    float* W1 = reinterpret_cast<float*>(Cf);                 // T lines
+
+    // ---- s = Dx + u_old ; w = z - u   (ops.jl:169-173) ----
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < NE) {
+            const int t = idx / M4;
+            const int i = (idx - t * M4) * 4;
+            const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+            const float4 xc = *reinterpret_cast<const float4*>(x + (t + 1) * M + i);
+            const float4 xp = *reinterpret_cast<const float4*>(x + t * M + i);
+            const float4 u0 = pre0[it];
+            float4 s0;
+            s0.x = (xc.x - xp.x) + clipf(u0.x, tau);
+            s0.y = (xc.y - xp.y) + clipf(u0.y, tau);
+            s0.z = (xc.z - xp.z) + clipf(u0.z, tau);
+            s0.w = (xc.w - xp.w) + clipf(u0.w, tau);
+            *reinterpret_cast<float4*>(W0 + t * M + i) =
+                make_float4(prox_w(s0.x, tau), prox_w(s0.y, tau), prox_w(s0.z, tau), prox_w(s0.w, tau));
+            if (t < T) {
+                const float xl = x[(t + 1) * M + ((i - 1) & (M - 1))];
+                const float4 u1 = pre1[it];
+                float4 s1;
+                s1.x = (xc.x - xl) + clipf(u1.x, tau);
+                s1.y = (xc.y - xc.x) + clipf(u1.y, tau);
+                s1.z = (xc.z - xc.y) + clipf(u1.z, tau);
+                s1.w = (xc.w - xc.z) + clipf(u1.w, tau);
+                *reinterpret_cast<float4*>(W1 + t * M + i) =
+                    make_float4(prox_w(s1.x, tau), prox_w(s1.y, tau), prox_w(s1.z, tau), prox_w(s1.w, tau));
+                *reinterpret_cast<float4*>(sn + off) = s0;
+                *reinterpret_cast<float4*>(sn + MN + off) = s1;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- v = H^T y + rho D^T w (ops.jl:168), fed straight into the forward pass 0 ----
+    float2* F0 = const_cast<float2*>(Xr);   // x is dead now
+#pragma unroll
+    for (int it = 0; it < NITF; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < T * QF) {
+            const int f = idx / QF, j = idx - f * QF;
+            const float* w0a = W0 + f * M;
+            const float* w0b = W0 + (f + 1) * M;
+            const float* w1 = W1 + f * M;
+            float2 v[RF];
+#pragma unroll
+            for (int r = 0; r < RF; ++r) {
+                const int n = j + r * QF;
+                const float2 a = *reinterpret_cast<const float2*>(w0a + 2 * n);
+                const float2 b = *reinterpret_cast<const float2*>(w0b + 2 * n);
+                const float2 c = *reinterpret_cast<const float2*>(w1 + 2 * n);
+                const float cn = w1[(2 * n + 2) & (M - 1)];
+                v[r].x = fmaf(rho, (a.x - b.x) + (c.x - c.y), preh[it][r].x);
+                v[r].y = fmaf(rho, (a.y - b.y) + (c.y - cn), preh[it][r].y);
+            }
+            fly_core<L, RF, 0, false, 2>(v, j, tw);
+            const int o = out_base<L, RF, 0>(j);
+            if constexpr (P == 1) {
+#pragma unroll
+                for (int r = 0; r < RF; ++r) F0[f * L + o + r] = v[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < RF; ++r) F0[f * L + o + r] = v[r];
+            }
+        }
+    }
+    __syncthreads();
+    float2* Z;
+    if constexpr (P == 1) {
+        Z = F0;
+    } else if constexpr (P == 2) {
+        float2* Zb = reinterpret_cast<float2*>(W0);   // w0 dead now
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{Zb, L});
+        __syncthreads();
+        Z = Zb;
+    } else {
+        float2* Zb = reinterpret_cast<float2*>(W0);
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{Zb, L});
+        __syncthreads();
+        plan_pass<L, 2, true, false, 2>(T, tw, LdsIO{Zb, L}, LdsIO{Cf, L});
+        __syncthreads();
+        Z = Cf;
+    }
+    pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
 }
 
 }  // namespace admm
