@@ -1,0 +1,186 @@
+"""ADMM deconvolution layers -- host-side mirror of /root/reference/src/layers/deconv_admm.jl.
+
+The reference defines four Flux layer types that differ only in which of (PSF weight, bias, λ, ρ)
+are trainable (`Flux.@layer ... trainable=`, deconv_admm.jl:55,107,161,209) and share one forward
+(deconv_admm.jl:215-225):
+
+    d.λ = clamp.(d.λ, d.creg, Inf32);  d.ρ = clamp.(d.ρ, d.creg, Inf32)   # written back
+    d.weight = clamp.(d.weight, 0f0, 1f0)                                   # written back
+    res = tvd_fft(x, d.λ, d.ρ, d.weight, d.iso, d.iters) .+ d.bias
+    return d.σ.(res)
+
+Here the parameters are torch tensors on a ROCm device and `tvd_fft` is the HIP solve behind the
+C ABI.  Shapes follow the rule "torch shape = reversed Julia shape": Julia weight (kh,kw,1,1) is
+torch (1,1,kw,kh); Julia input (M,N,P,B) is torch (B,P,N,M).  This round mirrors the forward
+(inference); the Zygote adjoint (BASELINE config c5) is the next step.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .ops import tvd_fft
+
+__all__ = ["ADMMDeconv", "ADMMDeconvF1", "ADMMDeconvF2", "ADMMDeconvF3", "Admm", "glorot_uniform",
+           "identity", "relu", "relu6", "relu1"]
+
+
+def identity(x):
+    return x
+
+
+def relu(x):
+    return torch.relu(x)
+
+
+def relu6(x):
+    return torch.clamp(x, 0.0, 6.0)
+
+
+def relu1(x):
+    return torch.clamp(x, 0.0, 1.0)
+
+
+def _nfan(dims):
+    """Flux.nfan: (fan_in, fan_out) for vector / matrix / conv-filter shapes (Julia order)."""
+    if len(dims) == 1:
+        return 1, dims[0]
+    if len(dims) == 2:
+        return dims[1], dims[0]
+    k = math.prod(dims[:-2])
+    return k * dims[-2], k * dims[-1]
+
+
+def glorot_uniform(*dims_julia, rng=None):
+    """Flux.glorot_uniform: (rand - 0.5) * sqrt(24 / (fan_in + fan_out)), float32, Julia dims.
+    Returns a numpy array in torch/C order (reversed dims)."""
+    rng = rng if rng is not None else np.random.default_rng()
+    fi, fo = _nfan(dims_julia)
+    a = (rng.random(tuple(reversed(dims_julia)), dtype=np.float64).astype(np.float32) - np.float32(0.5))
+    return (a * np.float32(math.sqrt(24.0 / (fi + fo)))).astype(np.float32)
+
+
+class Admm:
+    """Shared state and forward of the four ADMM layer types (`Admm` union, deconv_admm.jl:212)."""
+    TRAINABLE: tuple = ()
+
+    def __init__(self, sigma, weight, bias, lam, rho, iters, iso, creg, device=None):
+        dev = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        as_t = lambda v: torch.as_tensor(np.asarray(v, dtype=np.float32).reshape(-1), device=dev)  # noqa: E731
+        self.sigma = sigma if sigma is not None else identity
+        self.weight = torch.as_tensor(np.asarray(weight, dtype=np.float32), device=dev)
+        self.bias = False if bias is False or bias is None else as_t(bias)
+        self.lam = as_t(lam)
+        self.rho = as_t(rho)
+        self.iters = int(iters)
+        self.iso = bool(iso)
+        self.creg = float(creg)
+
+    # Flux.@layer ... trainable=(...)
+    def trainable(self):
+        return {name: getattr(self, name) for name in self.TRAINABLE}
+
+    @classmethod
+    def from_params(cls, w, sigma, b, lam, rho, iters, iso, creg, device=None):
+        """Positional constructor (deconv_admm.jl:18-28, :70-80, :122-132, :176-186)."""
+        return cls.__new__(cls)._init_raw(sigma, w, b, lam, rho, iters, iso, creg, device)
+
+    def _init_raw(self, *a, **k):
+        Admm.__init__(self, *a, **k)
+        return self
+
+    def to(self, device):
+        dev = torch.device(device)
+        self.weight = self.weight.to(dev)
+        self.lam = self.lam.to(dev)
+        self.rho = self.rho.to(dev)
+        if self.bias is not False:
+            self.bias = self.bias.to(dev)
+        return self
+
+    def __call__(self, x):
+        """(d::Admm)(x) -- deconv_admm.jl:215-225."""
+        self.lam = torch.clamp(self.lam, min=self.creg)          # :216 (written back)
+        self.rho = torch.clamp(self.rho, min=self.creg)          # :217
+        self.weight = torch.clamp(self.weight, 0.0, 1.0)         # :219
+        h = self.weight if self.weight.numel() > 0 else None
+        res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters)   # :221
+        if self.bias is not False:
+            res = res + self.bias                                 # :222
+        return self.sigma(res)                                    # :224
+
+    def __repr__(self):
+        k = tuple(reversed(self.weight.shape[-2:])) if self.weight.numel() else ()
+        return f"{type(self).__name__}({k}, {self.iters}, iso={self.iso})"
+
+
+def _psf(k, init, groups, rng):
+    if len(k) == 0:
+        return np.zeros((0,), np.float32)                          # empty(ones(1))
+    kh, kw = k
+    w = init(kh, kw, 1, 1, rng=rng) if init is glorot_uniform else np.asarray(init(kh, kw, 1, 1), np.float32)
+    return np.asarray(w, np.float32).reshape(1, 1, kw, kh)
+
+
+def _bias(bias):
+    if bias is False or bias is None:
+        return False                                               # Flux.create_bias(w, false, 1)
+    if bias is True:
+        return np.zeros(1, np.float32)
+    return np.asarray(bias, np.float32).reshape(-1)
+
+
+class ADMMDeconv(Admm):
+    """ADMMDeconv(k, num_it, σ=identity; iso, init, groups, bias, creg) -- deconv_admm.jl:189-209.
+    Trainable: weight, bias, λ, ρ; λ, ρ initialised abs.(glorot_uniform(1))."""
+    TRAINABLE = ("weight", "bias", "lam", "rho")
+
+    def __init__(self, k, num_it, sigma=identity, *, iso=False, init=glorot_uniform, groups=1, bias=False,
+                 creg=0.0, rng=None, device=None):
+        rng = rng if rng is not None else np.random.default_rng()
+        w = _psf(tuple(k), init, groups, rng)
+        lam = np.abs(glorot_uniform(1, rng=rng))
+        rho = np.abs(glorot_uniform(1, rng=rng))
+        super().__init__(sigma, w, _bias(bias), lam, rho, num_it, iso, creg, device)
+
+
+class ADMMDeconvF1(Admm):
+    """ADMMDeconvF1(k, num_it, λ, σ; ...) -- fixed λ (deconv_admm.jl:31-55). Trainable: weight, bias, ρ."""
+    TRAINABLE = ("weight", "bias", "rho")
+
+    def __init__(self, k, num_it, lam, sigma=identity, *, iso=False, init=glorot_uniform, groups=1, bias=False,
+                 creg=0.0, rng=None, device=None):
+        assert lam > 0.0, "Parameter λ must be greater than 0"       # :42
+        rng = rng if rng is not None else np.random.default_rng()
+        w = _psf(tuple(k), init, groups, rng)
+        rho = np.abs(glorot_uniform(1, rng=rng))
+        super().__init__(sigma, w, _bias(bias), [lam], rho, num_it, iso, creg, device)
+
+
+class ADMMDeconvF2(Admm):
+    """ADMMDeconvF2(k, num_it, ρ, σ; ...) -- fixed ρ (deconv_admm.jl:83-107). Trainable: weight, bias, λ."""
+    TRAINABLE = ("weight", "bias", "lam")
+
+    def __init__(self, k, num_it, rho, sigma=identity, *, iso=False, init=glorot_uniform, groups=1, bias=False,
+                 creg=0.0, rng=None, device=None):
+        assert rho > 0, "Parameter ρ must be greater than 0"          # :94
+        rng = rng if rng is not None else np.random.default_rng()
+        w = _psf(tuple(k), init, groups, rng)
+        lam = np.abs(glorot_uniform(1, rng=rng))
+        super().__init__(sigma, w, _bias(bias), lam, [rho], num_it, iso, creg, device)
+
+
+class ADMMDeconvF3(Admm):
+    """ADMMDeconvF3(k, num_it, λ, ρ, σ; ...) -- fixed λ and ρ (deconv_admm.jl:135-161). Trainable: weight, bias."""
+    TRAINABLE = ("weight", "bias")
+
+    def __init__(self, k, num_it, lam, rho, sigma=identity, *, iso=False, init=glorot_uniform, groups=1,
+                 bias=False, creg=0.0, rng=None, device=None):
+        assert lam > 0, "Parameter λ must be greater than 0"          # :147
+        assert rho > 0, "Parameter ρ must be greater than 0"          # :148
+        rng = rng if rng is not None else np.random.default_rng()
+        w = _psf(tuple(k), init, groups, rng)
+        super().__init__(sigma, w, _bias(bias), [lam], [rho], num_it, iso, creg, device)

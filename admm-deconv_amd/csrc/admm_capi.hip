@@ -38,12 +38,14 @@ int fail(int code, const char* fmt, ...) {
 bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 struct Layout {
-    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, total;
+    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, total;
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
-Layout make_layout(int M, int N, size_t planes, bool psf) {
+constexpr int kIsoGroup = 16;   // planes per ISO_A block (partial batch-norm sums)
+
+Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     Layout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -61,6 +63,8 @@ Layout make_layout(int M, int N, size_t planes, bool psf) {
     L.sB = take(planes * 2 * MN * 4);
     L.spec0 = take(planes * MN * 4);  // N lines x M/2 complex
     L.spec1 = take(planes * MN * 4);
+    L.fmap = iso ? take(MN * 4) : 0;
+    L.part = iso ? take(((planes + kIsoGroup - 1) / kIsoGroup) * MN * 4) : 0;
     L.total = off;
     return L;
 }
@@ -95,6 +99,8 @@ int column_KB(int M, int N) {
     return KB;
 }
 size_t column_lds(int N, int KB) { return (size_t)N * 16 + (size_t)KB * (N + 1) * 8; }
+size_t iso_a_lds(int M, int T) { return (size_t)M * 8 + 3 * (size_t)(T + 1) * (M / 2) * 8; }
+size_t iso_b_lds(int M, int T) { return (size_t)M * 8 + (size_t)(2 * T + 1) * M * 4 + 2 * (size_t)T * (M / 2) * 8; }
 
 // ---- profiler -------------------------------------------------------------------------------
 struct Prof {
@@ -205,6 +211,32 @@ int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* s
     return -1;
 }
 
+int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* so, float* sn,
+                 const float* fmap, float* part, const float2* twM, int N, int planes, int G, int sz) {
+#define X(l, t)                                                                                             \
+    if (L == l && T == t) {                                                                                 \
+        set_lds(iso_a_kernel<l, t>, lds);                                                                   \
+        iso_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, so, sn, fmap, part, twM, N, planes, G, sz);     \
+        return 0;                                                                                           \
+    }
+    ADMM_LT_CASES(X)
+#undef X
+    return -1;
+}
+
+int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* sn, const float* fmap,
+                 const float* hty, float2* spec0, const float2* twM, int N, float rho) {
+#define X(l, t)                                                                               \
+    if (L == l && T == t) {                                                                   \
+        set_lds(iso_b_kernel<l, t>, lds);                                                     \
+        iso_b_kernel<l, t><<<g, kThreads, lds, s>>>(sn, fmap, hty, spec0, twM, N, rho);      \
+        return 0;                                                                             \
+    }
+    ADMM_LT_CASES(X)
+#undef X
+    return -1;
+}
+
 int launch_column(int N, bool cplx, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
                   const float* C, const float2* G, const float2* twN, int L, int KB, float cs) {
 #define X(v)                                                                                 \
@@ -231,7 +263,8 @@ int check_shape(int M, int N, int P, int B, int kh, int kw, int iso) {
         return fail(ADMM_E_UNSUPPORTED, "this build supports power-of-two 4<=M<=1024, 2<=N<=1024 (got M=%d N=%d)", M, N);
     if (kh > M || kw > N)
         return fail(ADMM_E_UNSUPPORTED, "PSF %dx%d larger than the image (kh<=M, kw<=N required, as pad_constant in ops.jl:25)", kh, kw);
-    if (iso) return fail(ADMM_E_UNSUPPORTED, "isotropic (BT) prox is not in this build yet");
+    if (iso && (size_t)P * B > 65535)
+        return fail(ADMM_E_UNSUPPORTED, "isotropic prox couples the batch: at most 65535 planes per call");
     return ADMM_OK;
 }
 
@@ -247,7 +280,7 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    *out_bytes = make_layout(M, N, (size_t)P * B, kh > 0).total;
+    *out_bytes = make_layout(M, N, (size_t)P * B, kh > 0, iso != 0).total;
     return ADMM_OK;
 }
 
@@ -261,7 +294,7 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
     if (!std::isfinite(lambda) || !std::isfinite(rho)) return fail(ADMM_E_INVALID, "lambda and rho must be finite");
     const size_t planes = (size_t)P * B;
-    const Layout lay = make_layout(M, N, planes, kh > 0);
+    const Layout lay = make_layout(M, N, planes, kh > 0, iso != 0);
     if (!workspace || workspace_bytes < lay.total)
         return fail(ADMM_E_WORKSPACE, "workspace too small: need %zu bytes, got %zu", lay.total, workspace_bytes);
     if ((reinterpret_cast<uintptr_t>(workspace) & 255) != 0)
@@ -300,6 +333,8 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
     const int T = line_T(M, N);
     const int KB = column_KB(M, N);
     const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
+    float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
     const int kMaxY = 65535;
     for (size_t p0 = 0; p0 < planes; p0 += kMaxY) {
         const int np = (int)((planes - p0) < (size_t)kMaxY ? (planes - p0) : (size_t)kMaxY);
@@ -330,11 +365,28 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
                               it == 1 ? cs1 : 1.0f);
             });
             if (rc) return rc;
-            if (it < maxit) {
+            if (it < maxit && !iso) {
                 float* so = (it & 1) ? sb : sa;   // iteration 1 reads nothing (s_zero)
                 float* sn = (it & 1) ? sa : sb;
                 rc = ln.run(ADMM_K_LINE, [&] {
                     launch_line(L, T, gl, llds, s, sp1, sp0, so, sn, htyp, twM, N, tau, rho, it == 1 ? 1 : 0);
+                });
+            } else if (it < maxit) {
+                // isotropic: s is written in place (no halo reads of s in ISO_A)
+                const int ng = (np + kIsoGroup - 1) / kIsoGroup;
+                rc = ln.run(ADMM_K_LINE, [&] {
+                    launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, sp1, sa, sa, fmap, part, twM, N, np,
+                                 kIsoGroup, it == 1 ? 1 : 0);
+                });
+                if (rc) return rc;
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    const int nb = (int)((MN + kThreads - 1) / kThreads);
+                    hipLaunchKernelGGL(admm::iso_r_kernel, dim3(nb < 2048 ? nb : 2048), dim3(kThreads), 0, s, part,
+                                       fmap, ng, MN, tau);
+                });
+                if (rc) return rc;
+                rc = ln.run(ADMM_K_LINE, [&] {
+                    launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sa, fmap, htyp, sp0, twM, N, rho);
                 });
             } else {
                 rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, sp1, xp, twM, N); });

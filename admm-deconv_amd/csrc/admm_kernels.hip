@@ -542,4 +542,208 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
 }
 
+// ----------------------------------------------------------------------------------------------
+// ISOTROPIC (block-thresholding) path, ops.jl:6,10.  pixelnorm sums s^2 over BOTH channels of EVERY
+// plane of the batch, so the prox needs a batch-wide reduction between computing s and using it:
+//   ISO_A  (per line tile, G planes per block): irFFT -> x -> s = Dx + u_old -> write s, and the
+//          partial per-pixel sum of s0^2 + s1^2 over the block's G planes (no atomics)
+//   ISO_R  (per pixel): n = sqrt(sum of partials); f = max(1 - tau/n, 0) with Julia's NaN
+//          propagation (tau = 0 and n = 0 gives NaN, as the reference does)
+//   ISO_B  (per line tile): z = f s, u = s - z, w = z - u -> v = H^T y + rho D^T w -> rFFT
+// u_old for the next iteration is s - f s with the SAME f (kept in the workspace).
+// ----------------------------------------------------------------------------------------------
+__device__ __forceinline__ float max0_nan(float a) { return a != a ? a : fmaxf(a, 0.0f); }
+
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restrict__ spec1,
+                                                         const float* s_old, float* s_new,
+                                                         const float* __restrict__ fmap, float* __restrict__ part,
+                                                         const float2* __restrict__ twM, int N, int planes, int G,
+                                                         int s_zero) {
+    constexpr int M = 2 * L;
+    constexpr int M4 = M / 4;
+    constexpr int TH = T + 1;           // one halo line on the left (x[j-1])
+    constexpr int NE = T * M4;
+    constexpr int NIT = (NE + kThreads - 1) / kThreads;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float2* X = tw + M;
+    float2* Bf = X + TH * L;
+    float2* Cf = Bf + TH * L;
+    const int j0 = blockIdx.x * T;
+    const int grp = blockIdx.y;
+    const size_t MN = (size_t)M * N;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    float4 acc[NIT], fo[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        acc[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int idx = tid + it * kThreads;
+        const int t = idx / M4, i = (idx - t * M4) * 4;
+        fo[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!s_zero && idx < NE) fo[it] = *reinterpret_cast<const float4*>(fmap + (size_t)(j0 + t) * M + i);
+    }
+    const int p_end = min(planes, (grp + 1) * G);
+    for (int plane = grp * G; plane < p_end; ++plane) {
+        __syncthreads();   // previous plane's LDS readers are done
+        load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
+        __syncthreads();
+        auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
+        float2* Xr;
+        if constexpr (Plan<L>::P == 1) {
+            Xr = Bf;
+            fpass<L, L, 0, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+        } else if constexpr (Plan<L>::P == 2) {
+            Xr = X;
+            fft_plan<L, false, true, 2>(TH, tw, Bf, Cf, L, uload, LdsIO{X, L});
+        } else {
+            Xr = Bf;
+            plan_pass<L, 0, false, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+            __syncthreads();
+            plan_pass<L, 1, false, true, 2>(TH, tw, LdsIO{Bf, L}, LdsIO{Cf, L});
+            __syncthreads();
+            plan_pass<L, 2, false, true, 2>(TH, tw, LdsIO{Cf, L}, LdsIO{Bf, L});
+        }
+        __syncthreads();
+        const float* x = reinterpret_cast<const float*>(Xr);
+        const float* so = s_old + (size_t)plane * 2 * MN;
+        float* sn = s_new + (size_t)plane * 2 * MN;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int idx = tid + it * kThreads;
+            if (idx < NE) {
+                const int t = idx / M4, i = (idx - t * M4) * 4;
+                const size_t off = (size_t)(j0 + t) * M + i;
+                const float4 xc = *reinterpret_cast<const float4*>(x + (t + 1) * M + i);
+                const float4 xp = *reinterpret_cast<const float4*>(x + t * M + i);
+                const float xl = x[(t + 1) * M + ((i - 1) & (M - 1))];
+                float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+                if (!s_zero) {
+                    a0 = *reinterpret_cast<const float4*>(so + off);
+                    a1 = *reinterpret_cast<const float4*>(so + MN + off);
+                }
+                const float4 f = fo[it];
+                // u_old = s_old - f s_old   (f from the previous iteration's batch norm)
+                float4 s0, s1;
+                s0.x = (xc.x - xp.x) + (a0.x - f.x * a0.x);
+                s0.y = (xc.y - xp.y) + (a0.y - f.y * a0.y);
+                s0.z = (xc.z - xp.z) + (a0.z - f.z * a0.z);
+                s0.w = (xc.w - xp.w) + (a0.w - f.w * a0.w);
+                s1.x = (xc.x - xl) + (a1.x - f.x * a1.x);
+                s1.y = (xc.y - xc.x) + (a1.y - f.y * a1.y);
+                s1.z = (xc.z - xc.y) + (a1.z - f.z * a1.z);
+                s1.w = (xc.w - xc.z) + (a1.w - f.w * a1.w);
+                *reinterpret_cast<float4*>(sn + off) = s0;
+                *reinterpret_cast<float4*>(sn + MN + off) = s1;
+                acc[it].x += s0.x * s0.x + s1.x * s1.x;
+                acc[it].y += s0.y * s0.y + s1.y * s1.y;
+                acc[it].z += s0.z * s0.z + s1.z * s1.z;
+                acc[it].w += s0.w * s0.w + s1.w * s1.w;
+            }
+        }
+    }
+    float* pp = part + (size_t)grp * MN;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        const int idx = tid + it * kThreads;
+        if (idx < NE) {
+            const int t = idx / M4, i = (idx - t * M4) * 4;
+            *reinterpret_cast<float4*>(pp + (size_t)(j0 + t) * M + i) = acc[it];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
+                                                         int ngroups, size_t MN, float tau) {
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
+        float acc = 0.0f;
+        for (int g = 0; g < ngroups; ++g) acc += part[(size_t)g * MN + q];
+        fmap[q] = max0_nan(1.0f - tau / sqrtf(acc));   // BT factor, ops.jl:10
+    }
+}
+
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict__ s_new, const float* __restrict__ fmap,
+                                                         const float* __restrict__ hty, float2* __restrict__ spec0,
+                                                         const float2* __restrict__ twM, int N, float rho) {
+    constexpr int M = 2 * L;
+    constexpr int M4 = M / 4;
+    constexpr int P = Plan<L>::P;
+    constexpr int RF = plan_radix<L, 0, true>();
+    constexpr int QF = L / RF;
+    constexpr int NE = (T + 1) * M4;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float* W0 = reinterpret_cast<float*>(tw + M);   // T+1 lines
+    float* W1 = W0 + (T + 1) * M;                   // T lines
+    float2* F0 = reinterpret_cast<float2*>(W1 + T * M);   // T lines
+    float2* F1 = F0 + T * L;                               // T lines
+    const int plane = blockIdx.y;
+    const int j0 = blockIdx.x * T;
+    const size_t MN = (size_t)M * N;
+    const int tid = threadIdx.x;
+    const float* sp = s_new + (size_t)plane * 2 * MN;
+    const float* hp = hty + (size_t)plane * MN;
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    for (int idx = tid; idx < NE; idx += kThreads) {
+        const int t = idx / M4, i = (idx - t * M4) * 4;
+        const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+        const float4 f = *reinterpret_cast<const float4*>(fmap + off);
+        const float4 a = *reinterpret_cast<const float4*>(sp + off);
+        float4 w;
+        // z = f s ; u = s - z ; w = z - u
+        w.x = f.x * a.x - (a.x - f.x * a.x);
+        w.y = f.y * a.y - (a.y - f.y * a.y);
+        w.z = f.z * a.z - (a.z - f.z * a.z);
+        w.w = f.w * a.w - (a.w - f.w * a.w);
+        *reinterpret_cast<float4*>(W0 + t * M + i) = w;
+        if (t < T) {
+            const float4 b = *reinterpret_cast<const float4*>(sp + MN + off);
+            w.x = f.x * b.x - (b.x - f.x * b.x);
+            w.y = f.y * b.y - (b.y - f.y * b.y);
+            w.z = f.z * b.z - (b.z - f.z * b.z);
+            w.w = f.w * b.w - (b.w - f.w * b.w);
+            *reinterpret_cast<float4*>(W1 + t * M + i) = w;
+        }
+    }
+    __syncthreads();
+    for (int idx = tid; idx < T * QF; idx += kThreads) {
+        const int f = idx / QF, j = idx - f * QF;
+        const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
+        float2 v[RF];
+#pragma unroll
+        for (int r = 0; r < RF; ++r) {
+            const int n = j + r * QF;
+            const float2 hv = hl[n];
+            const float2 a = *reinterpret_cast<const float2*>(W0 + f * M + 2 * n);
+            const float2 b = *reinterpret_cast<const float2*>(W0 + (f + 1) * M + 2 * n);
+            const float2 c = *reinterpret_cast<const float2*>(W1 + f * M + 2 * n);
+            const float cn = W1[f * M + ((2 * n + 2) & (M - 1))];
+            v[r].x = fmaf(rho, (a.x - b.x) + (c.x - c.y), hv.x);
+            v[r].y = fmaf(rho, (a.y - b.y) + (c.y - cn), hv.y);
+        }
+        fly_core<L, RF, 0, false, 2>(v, j, tw);
+        const int o = out_base<L, RF, 0>(j);
+#pragma unroll
+        for (int r = 0; r < RF; ++r) F0[f * L + o + r] = v[r];
+    }
+    __syncthreads();
+    float2* Z;
+    if constexpr (P == 1) {
+        Z = F0;
+    } else if constexpr (P == 2) {
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{F1, L});
+        __syncthreads();
+        Z = F1;
+    } else {
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{F1, L});
+        __syncthreads();
+        plan_pass<L, 2, true, false, 2>(T, tw, LdsIO{F1, L}, LdsIO{F0, L});
+        __syncthreads();
+        Z = F0;
+    }
+    pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
+}
+
 }  // namespace admm

@@ -1,0 +1,66 @@
+"""The layer mirror (src/layers/deconv_admm.jl) on the GPU against the oracle's restated forward."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_np
+from admm_deconv import layers, synth
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_layer(layer, y):
+    w = layer.weight.detach().cpu().numpy()
+    w = None if w.size == 0 else oracle_np.psf_from_c(w.reshape(w.shape[-2:]))
+    bias = None if layer.bias is False else layer.bias.cpu().numpy()
+    x = oracle_np.admm_layer_forward(oracle_np.from_c(y.astype(np.float64)), layer.lam.item(), layer.rho.item(), w,
+                                     layer.iso, layer.iters, layer.creg, bias, None)
+    return oracle_np.to_c(x)
+
+
+@pytest.mark.parametrize("kind", ["ADMMDeconv", "F1", "F2", "F3", "F2-empty", "F3-iso-bias"])
+def test_layer_forward(dev, kind):
+    rng = np.random.default_rng(5)
+    if kind == "ADMMDeconv":
+        L = layers.ADMMDeconv((10, 10), 12, layers.relu, rng=rng, device=dev)
+    elif kind == "F1":
+        L = layers.ADMMDeconvF1((7, 7), 10, 0.004, rng=rng, device=dev)
+    elif kind == "F2":
+        L = layers.ADMMDeconvF2((7, 7), 10, 0.04, layers.relu6, rng=rng, device=dev)
+    elif kind == "F2-empty":
+        L = layers.ADMMDeconvF2((), 50, 0.02, layers.relu1, rng=rng, device=dev)   # net_build.jl:115
+    elif kind == "F3":
+        L = layers.ADMMDeconvF3((15, 15), 25, 0.0041, 0.021, rng=rng, device=dev)
+    else:
+        L = layers.ADMMDeconvF3((9, 9), 10, 0.01, 0.05, iso=True, bias=True, rng=rng, device=dev)
+        L.bias = L.bias + 0.25
+    y = synth.make_batch(3, 64, 64, synth.gaussian_psf(9, 1.2), P=2)
+    out = L(torch.from_numpy(y).to(dev))
+    torch.cuda.synchronize()
+    # the forward wrote the projected parameters back (deconv_admm.jl:216-219)
+    assert L.weight.numel() == 0 or (float(L.weight.min()) >= 0.0 and float(L.weight.max()) <= 1.0)
+    assert float(L.lam.min()) >= L.creg and float(L.rho.min()) >= L.creg
+    ref = oracle_layer(L, y)
+    act = {"ADMMDeconv": lambda a: np.maximum(a, 0), "F2": lambda a: np.clip(a, 0, 6),
+           "F2-empty": lambda a: np.clip(a, 0, 1)}.get(kind, lambda a: a)
+    got = out.cpu().numpy()
+    ref = act(ref)
+    if kind in ("ADMMDeconv", "F2", "F2-empty"):
+        # activations clip; compare with an absolute guard scaled by the pre-activation magnitude
+        assert np.abs(got - ref).max() <= 2e-4 * max(1.0, np.abs(ref).max())
+    else:
+        assert_parity(got, ref, what=kind)
+
+
+def test_trainable_sets():
+    assert layers.ADMMDeconv.TRAINABLE == ("weight", "bias", "lam", "rho")       # deconv_admm.jl:209
+    assert layers.ADMMDeconvF1.TRAINABLE == ("weight", "bias", "rho")            # :55
+    assert layers.ADMMDeconvF2.TRAINABLE == ("weight", "bias", "lam")            # :107
+    assert layers.ADMMDeconvF3.TRAINABLE == ("weight", "bias")                   # :161
+
+
+def test_creg_clamp(dev):
+    L = layers.ADMMDeconvF3((5, 5), 3, 0.001, 0.002, creg=0.01, device=dev)
+    L(torch.from_numpy(synth.make_batch(1, 32, 32, None)).to(dev))
+    assert abs(L.lam.item() - 0.01) < 1e-7 and abs(L.rho.item() - 0.01) < 1e-7

@@ -95,3 +95,34 @@ def test_batch_sharding_invariance(dev):
                      + [admm_deconv.tvd_fft(y[6:].contiguous(), 0.0041, 0.021, ht, False, 6)])
     torch.cuda.synchronize()
     assert torch.equal(full, part)
+
+
+ISO_CASES = [
+    # (B, P, N, M, psf, lam, rho, K)
+    (4, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 10),
+    (2, 3, 32, 64, None, 0.05, 0.02, 8),                        # RGB denoiser, iso (train_cfg use_iso)
+    (3, 1, 128, 128, ("rand", 10, 10), 0.02, 0.1, 6),
+    (40, 1, 16, 16, ("gauss", 5, 1.0), 0.01, 0.05, 5),          # > one ISO_A plane group
+    (2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
+]
+
+
+@pytest.mark.parametrize("case", ISO_CASES, ids=[f"iso-{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}" for c in ISO_CASES])
+def test_iso_parity_vs_oracle(dev, case):
+    B, P, N, M, psf, lam, rho, K = case
+    rng = np.random.default_rng(B * 7 + N + K)
+    h = make_psf(psf, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=3)
+    got = run_gpu(dev, y, lam, rho, h, True, K)
+    ref = run_oracle(y, lam, rho, h, True, K)
+    assert_parity(got, ref, what="iso " + str(case))
+
+
+def test_iso_couples_batch(dev):
+    """pixelnorm sums over the whole batch (ops.jl:6): the iso result of a plane depends on its batch."""
+    h = synth.gaussian_psf(7, 1.5)
+    y = synth.make_batch(4, 32, 32, h)
+    full = run_gpu(dev, y, 0.05, 0.05, h, True, 6)
+    alone = run_gpu(dev, y[:1], 0.05, 0.05, h, True, 6)
+    assert not np.allclose(full[:1], alone, rtol=0, atol=1e-6)
+    assert_parity(alone, run_oracle(y[:1], 0.05, 0.05, h, True, 6))
