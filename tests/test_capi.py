@@ -1,0 +1,71 @@
+"""CPU: the C-ABI library loads, exports every symbol include/admm_deconv.h declares, and validates
+arguments (no GPU compute is issued by these calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from admm_deconv import _lib
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "admm_deconv.h")
+
+
+def header_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(admm_\w+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert header_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    L = _lib.load()
+    for name in header_functions():
+        assert hasattr(L, name), name
+    assert L.admm_abi_version() == 1
+
+
+def test_workspace_bytes():
+    n1 = _lib.workspace_bytes(256, 256, 1, 512, 15, 15, False)
+    n0 = _lib.workspace_bytes(256, 256, 1, 512, 0, 0, False)
+    assert n1 > n0 >= 512 * 256 * 256 * 4 * 6
+    assert _lib.workspace_bytes(256, 256, 1, 512, 15, 15, True) > n1
+
+
+@pytest.mark.parametrize("args,code", [
+    ((48, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),   # non-power-of-two M
+    ((64, 2048, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large
+    ((64, 64, 1, 1, 5, 0, 0), _lib.ADMM_E_INVALID),        # half-empty PSF
+    ((64, 64, 0, 1, 5, 5, 0), _lib.ADMM_E_INVALID),        # P = 0
+    ((64, 64, 1, 1, 65, 5, 0), _lib.ADMM_E_UNSUPPORTED),   # PSF taller than the image
+])
+def test_workspace_validation(args, code):
+    out = ctypes.c_size_t(0)
+    assert _lib.load().admm_tvd_workspace_bytes(*args, ctypes.byref(out)) == code
+    assert len(_lib.load().admm_last_error()) > 0
+
+
+def test_forward_argument_errors_before_any_device_work():
+    L = _lib.load()
+    fake = 1 << 20   # never dereferenced: validation fails first
+    assert L.admm_tvd_forward_f32(None, fake, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0, 0, 5, fake, 1 << 30, None) \
+        == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_forward_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0, 0, -1, fake, 1 << 30, None) \
+        == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_forward_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, float("nan"), 1.0, 0, 5, fake, 1 << 30,
+                                  None) == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_forward_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0, 0, 5, fake, 16, None) \
+        == _lib.ADMM_E_WORKSPACE
+    assert L.admm_tvd_forward_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0, 0, 5, fake + 8, 1 << 30, None) \
+        == _lib.ADMM_E_WORKSPACE
+    assert b"workspace" in L.admm_last_error()
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+    from admm_deconv import tvd_fft
+    with pytest.raises(TypeError):
+        tvd_fft(torch.zeros(1, 1, 8, 8), 0.1, 1.0)
