@@ -1,0 +1,49 @@
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes per kernel class.
+
+usage: python tools/make_traffic.py CONFIG OUT.json gpurun_out/prof_TAG/pmc_fetch gpurun_out/prof_TAG/pmc_write
+
+hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (FETCH_SIZE reads half the bytes of
+a wide coalesced stream on gfx950 -- MI355X_MICROARCH.md, HBM section; WRITE_SIZE is exact for 16-B
+stores).  Infinity-Cache hits are counted too (same section).  Values merge into OUT.json[CONFIG].
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import load  # noqa: E402
+
+CLASS = {"line_kernel": "line", "column_kernel<256, false>": "column", "iso_a_kernel": "iso_a",
+         "iso_b_kernel": "iso_b", "plane_kernel": "plane"}
+
+
+def klass(name):
+    for k, v in CLASS.items():
+        if name.startswith(k):
+            return v
+    if name.startswith("column_kernel") and "false" in name:
+        return "column"
+    return None
+
+
+def main():
+    cfg, out, fdir, wdir = sys.argv[1:5]
+    f = load([fdir])
+    w = load([wdir])
+    res = json.load(open(out)) if os.path.exists(out) else {}
+    ent = res.setdefault(cfg, {})
+    for name in f:
+        c = klass(name)
+        if c is None or name not in w:
+            continue
+        fs = sum(f[name]["FETCH_SIZE"]) / len(f[name]["FETCH_SIZE"])
+        ws = sum(w[name]["WRITE_SIZE"]) / len(w[name]["WRITE_SIZE"])
+        ent[c] = {"kernel": name, "fetch_size_kib": fs, "write_size_kib": ws,
+                  "hbm_bytes_per_launch": int(2 * fs * 1024 + ws * 1024),
+                  "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 correction); includes Infinity-Cache hits"}
+        print(cfg, c, ent[c]["hbm_bytes_per_launch"])
+    json.dump(res, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
