@@ -23,6 +23,7 @@ KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: 
 
 # Every symbol include/admm_deconv.h declares (checked by tests/test_capi.py).
 EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "admm_tvd_forward_f32",
+           "admm_tvd_backward_workspace_bytes", "admm_tvd_backward_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
 
 
@@ -58,6 +59,12 @@ def load():
     L.admm_tvd_forward_f32.restype = c_int
     L.admm_tvd_forward_f32.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                                        c_float, c_float, c_int, c_int, c_void_p, c_size_t, c_void_p]
+    L.admm_tvd_backward_workspace_bytes.restype = c_int
+    L.admm_tvd_backward_workspace_bytes.argtypes = [c_int] * 9 + [ctypes.POINTER(c_size_t)]
+    L.admm_tvd_backward_f32.restype = c_int
+    L.admm_tvd_backward_f32.argtypes = [c_void_p] * 6 + [c_int] * 4 + [c_void_p, c_int, c_int, c_float, c_float,
+                                                                         c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                                                         c_void_p]
     L.admm_profile_enable.restype = c_int
     L.admm_profile_enable.argtypes = [c_int]
     L.admm_profile_reset.restype = c_int
@@ -77,6 +84,13 @@ def check(rc):
 def workspace_bytes(M, N, P, B, kh, kw, iso):
     out = ctypes.c_size_t(0)
     check(load().admm_tvd_workspace_bytes(M, N, P, B, kh, kw, int(bool(iso)), ctypes.byref(out)))
+    return out.value
+
+
+def backward_workspace_bytes(M, N, P, B, kh, kw, iso, maxit, want_hbar):
+    out = ctypes.c_size_t(0)
+    check(load().admm_tvd_backward_workspace_bytes(M, N, P, B, kh, kw, int(bool(iso)), int(maxit),
+                                                   int(bool(want_hbar)), ctypes.byref(out)))
     return out.value
 
 

@@ -103,9 +103,12 @@ class Admm:
 
     def __call__(self, x):
         """(d::Admm)(x) -- deconv_admm.jl:215-225."""
-        self.lam = torch.clamp(self.lam, min=self.creg)          # :216 (written back)
-        self.rho = torch.clamp(self.rho, min=self.creg)          # :217
-        self.weight = torch.clamp(self.weight, 0.0, 1.0)         # :219
+        # projection written back into the layer (deconv_admm.jl:216-219); in place on the leaf
+        # parameters so that, like Zygote on the reference, gradients reach the stored tensors
+        with torch.no_grad():
+            self.lam.clamp_(min=self.creg)                       # :216
+            self.rho.clamp_(min=self.creg)                       # :217
+            self.weight.clamp_(0.0, 1.0)                         # :219
         h = self.weight if self.weight.numel() > 0 else None
         res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters)   # :221
         if self.bias is not False:

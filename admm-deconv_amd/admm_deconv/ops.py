@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["tvd_fft", "Workspace"]
+__all__ = ["tvd_fft", "tvd_fft_backward", "Workspace"]
 
 
 class Workspace:
@@ -52,7 +52,7 @@ def _scalar(v, name):
     return v
 
 
-def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None):
+def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None):
     """ADMM TV deconvolution of every (M x N) plane of y (ops.jl:181).
 
     y:    torch float32 tensor (B, P, N, M) on a ROCm device (Julia (M,N,P,B)); a 2-D (N, M) or
@@ -103,3 +103,87 @@ def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, wo
         y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, int(bool(isotropic)), int(maxit),
         ws_ptr, ws_len, s_handle))
     return out.reshape(shape)
+
+
+def _prep(y, h):
+    if not isinstance(y, torch.Tensor) or y.device.type != "cuda" or y.dtype != torch.float32:
+        raise TypeError("y must be a float32 torch tensor on a ROCm device (no CPU path in this package)")
+    shape = y.shape
+    y4 = y.reshape((1,) * (4 - y.dim()) + tuple(shape)).contiguous() if y.dim() < 4 else y.contiguous()
+    if h is None or h.numel() == 0:
+        return shape, y4, None
+    hb = h.detach()
+    while hb.dim() > 2 and hb.shape[0] == 1:
+        hb = hb[0]
+    return shape, y4, hb.to(device=y.device, dtype=torch.float32).contiguous()
+
+
+def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, workspace=None,
+                     stream=None):
+    """Adjoint of tvd_fft through all `maxit` unrolled iterations (what Zygote computes for the
+    reference, src/train.jl:51).  Returns (x, y_bar, h_bar, lam_bar, rho_bar); h_bar is None without a PSF
+    or when need_h is False.  Recomputes the forward (x is returned for convenience)."""
+    shape, y4, hb = _prep(y, h)
+    B, P, N, M = y4.shape
+    xb = x_bar.reshape(y4.shape).to(torch.float32).contiguous()
+    lam = _scalar(lam, "lambda")
+    rho = _scalar(rho, "rho")
+    kw, kh = (0, 0) if hb is None else hb.shape
+    want_h = need_h and hb is not None
+    nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, want_h)
+    if workspace is None:
+        workspace = _default_ws.setdefault(("bwd", y.device), Workspace())
+    ws_ptr, ws_len = workspace.get(nbytes, y.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(y.device)
+    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    x = torch.empty_like(y4)
+    y_bar = torch.empty_like(y4)
+    h_bar = torch.empty_like(hb) if want_h else None
+    scal = torch.zeros(2, dtype=torch.float32, device=y.device)
+    _lib.check(_lib.load().admm_tvd_backward_f32(
+        y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
+        scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, lam, rho,
+        int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle))
+    return x.reshape(shape), y_bar.reshape(shape), h_bar, scal[0], scal[1]
+
+
+class _TvdFFTFn(torch.autograd.Function):
+    """Differentiable tvd_fft: forward through the HIP solve, backward through the HIP adjoint
+    (the rrule the Julia shim would register, julia/ADMMDeconvHIP.jl)."""
+
+    @staticmethod
+    def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit):
+        ctx.save_for_backward(y, lam_t, rho_t, h_t)
+        ctx.iso, ctx.maxit = isotropic, maxit
+        return _forward_raw(y, lam_t, rho_t, h_t, isotropic, maxit)
+
+    @staticmethod
+    def backward(ctx, x_bar):
+        y, lam_t, rho_t, h_t = ctx.saved_tensors
+        need_h = h_t is not None and h_t.numel() > 0 and ctx.needs_input_grad[3]
+        _, yb, hb, lb, rb = tvd_fft_backward(y, x_bar, lam_t, rho_t, h_t if h_t.numel() else None, ctx.iso,
+                                             ctx.maxit, need_h=need_h)
+        hg = None
+        if need_h:
+            hg = hb.reshape(h_t.shape)
+        return (yb if ctx.needs_input_grad[0] else None,
+                lb.reshape(lam_t.shape).to(lam_t.dtype) if ctx.needs_input_grad[1] else None,
+                rb.reshape(rho_t.shape).to(rho_t.dtype) if ctx.needs_input_grad[2] else None,
+                hg, None, None)
+
+
+def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None):
+    """ADMM TV deconvolution of every (M x N) plane of y -- src/ops/ops.jl:181 semantics.
+
+    y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: scalars or
+    1-element tensors; h: PSF (kw,kh) (= Julia (kh,kw)) or None/empty.  Returns a new tensor.
+    Differentiable (y, lam, rho, h) when autograd is recording and any of them requires grad
+    (anisotropic prox); the gradient is the exact adjoint of the K unrolled iterations."""
+    tensors = [t for t in (y, lam, rho, h) if isinstance(t, torch.Tensor)]
+    if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
+        dev = y.device
+        as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.tensor([float(v)], device=dev)  # noqa: E731
+        h_t = h if isinstance(h, torch.Tensor) else torch.zeros(0, device=dev)
+        return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit))
+    return _forward_raw(y, lam, rho, h, isotropic, maxit, out=out, workspace=workspace, stream=stream)

@@ -1,0 +1,341 @@
+// admm_backward.hip -- adjoint of the anisotropic ADMM solve (BASELINE c5).
+//
+// The reference differentiates tvd_fft by letting Zygote unroll all K iterations
+// (src/train.jl:51, src/ADMM_Deconv.jl:12-13), keeping every iteration's temporaries.  Here the
+// forward stores one state tensor per iteration (s_k, 8 B/px) and the reverse sweep runs the same
+// two-pass structure backwards (tests/kernel_model.py tvd_model_grads is the restatement, checked
+// against PyTorch autograd of oracle/oracle_torch.py):
+//
+//   step k = K..1:  vbar_k = A^-1 g_k                       (column pass; A^-1 is symmetric)
+//                   Dvb = D vbar_k
+//                   rho_bar += -<Dvb, D x_k>                (x_k's dependence on rho through A)
+//                   k >= 2: wbar = rho Dvb, rho_bar += <phi(s_{k-1}), Dvb>     (rho D^T w term)
+//                           sbar_{k-1} = phi'(s_{k-1}) wbar + psi'(s_{k-1}) sbar_k
+//                           tau_bar  += dphi/dtau wbar + dpsi/dtau sbar_k
+//                           g_{k-1} = D^T sbar_{k-1}  -> rFFT along dim 1 (next column pass)
+//                   Vsum += vbar_k
+// with phi(s) = ST(s) - clip(s) (= z - u) and psi(s) = clip(s) (= u).  Afterwards
+//   y_bar = H Vsum,   h_bar = <Vsum, dH^T y/dh> - (1/MN) sum_nu C^2 Q d|Sigma|^2/dh,
+//   lam_bar = tau_bar / rho,   rho_bar -= tau_bar lam / rho^2,
+// where Q[nu] = sum_k Re(conj(G_k) V_k) is accumulated by the column pass against the forward
+// spectra saved in the trajectory (only when h_bar is requested).
+#include <hip/hip_runtime.h>
+
+namespace admm {
+
+__device__ __forceinline__ float sgnf(float s) { return (s > 0.f) - (s < 0.f); }
+__device__ __forceinline__ float phi_f(float s, float tau) { return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s; }
+
+// block-wide reduction of two floats into doubles; lane 0 of the block writes them
+__device__ __forceinline__ void block_sum2(float a, float b, double* out, double* red) {
+    double da = a, db = b;
+    for (int off = 32; off > 0; off >>= 1) {
+        da += __shfl_down(da, off);
+        db += __shfl_down(db, off);
+    }
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) { red[2 * w] = da; red[2 * w + 1] = db; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sa = 0.0, sb = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { sa += red[2 * i]; sb += red[2 * i + 1]; }
+        out[0] = sa;
+        out[1] = sb;
+    }
+}
+
+// ----------------------------------------------------------------------------------------------
+// LINE_ADJ: one reverse step's line work for T lines (+1 halo line each side of vbar).
+//   spec1  : line spectrum of vbar_k (output of the adjoint column pass)
+//   sk1    : s_{k-1} (trajectory; null for k = 1)      sk : s_k (null for k = K)
+//   xK     : forward output x_K (used only at k = K for D x_K)
+//   sb_in  : sbar_k (null at k = K: zero)              sb_out : sbar_{k-1}
+//   vsum   : running sum of vbar (read-modify-write)   spec0 : rFFT_dim1 of g_{k-1}
+//   part   : per-block (rho_bar, tau_bar) partial sums
+// ----------------------------------------------------------------------------------------------
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __restrict__ spec1,
+                                                            const float* __restrict__ sk1, const float* __restrict__ sk,
+                                                            const float* __restrict__ xK,
+                                                            const float* __restrict__ sb_in, float* __restrict__ sb_out,
+                                                            float* __restrict__ vsum, float2* __restrict__ spec0,
+                                                            double* __restrict__ part, const float2* __restrict__ twM,
+                                                            int N, float tau, float rho, int first_k /*k==1*/,
+                                                            int last_k /*k==K*/) {
+    constexpr int M = 2 * L;
+    constexpr int M4 = M / 4;
+    constexpr int TH = T + 2;
+    constexpr int P = Plan<L>::P;
+    constexpr int RF = plan_radix<L, 0, true>();
+    constexpr int QF = L / RF;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float2* X = tw + M;
+    float2* Bf = X + TH * L;
+    float2* Cf = Bf + TH * L;
+    double* red = reinterpret_cast<double*>(Cf + TH * L);   // 2 doubles per wave
+    const int plane = blockIdx.y;
+    const int j0 = blockIdx.x * T;
+    const size_t MN = (size_t)M * N;
+    const int tid = threadIdx.x;
+    const size_t poff = (size_t)plane * 2 * MN;
+
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
+    __syncthreads();
+    auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
+    float2* Xr;
+    if constexpr (P == 1) {
+        Xr = Bf;
+        fpass<L, L, 0, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+    } else if constexpr (P == 2) {
+        Xr = X;
+        fft_plan<L, false, true, 2>(TH, tw, Bf, Cf, L, uload, LdsIO{X, L});
+    } else {
+        Xr = Bf;
+        plan_pass<L, 0, false, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+        __syncthreads();
+        plan_pass<L, 1, false, true, 2>(TH, tw, LdsIO{Bf, L}, LdsIO{Cf, L});
+        __syncthreads();
+        plan_pass<L, 2, false, true, 2>(TH, tw, LdsIO{Cf, L}, LdsIO{Bf, L});
+    }
+    __syncthreads();
+    const float* vb = reinterpret_cast<const float*>(Xr);       // vbar lines j0-1 .. j0+T
+    float* SB0 = reinterpret_cast<float*>(Xr == X ? Bf : X);    // sbar_{k-1} ch0, lines j0..j0+T
+    float* SB1 = reinterpret_cast<float*>(Cf);                  // sbar_{k-1} ch1, lines j0..j0+T-1
+
+    float rho_acc = 0.0f, tau_acc = 0.0f;
+    for (int idx = tid; idx < (T + 1) * M4; idx += kThreads) {
+        const int t = idx / M4;
+        const int i = (idx - t * M4) * 4;
+        const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+        const float4 vc = *reinterpret_cast<const float4*>(vb + (t + 1) * M + i);
+        const float4 vp = *reinterpret_cast<const float4*>(vb + t * M + i);
+        const float vl = vb[(t + 1) * M + ((i - 1) & (M - 1))];
+        const float dv0[4] = {vc.x - vp.x, vc.y - vp.y, vc.z - vp.z, vc.w - vp.w};
+        const float dv1[4] = {vc.x - vl, vc.y - vc.x, vc.z - vc.y, vc.w - vc.z};
+        const bool own = t < T;
+        float s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};   // s_{k-1}
+        if (!first_k) {
+            const float4 a = *reinterpret_cast<const float4*>(sk1 + poff + off);
+            s0[0] = a.x; s0[1] = a.y; s0[2] = a.z; s0[3] = a.w;
+            if (own) {
+                const float4 b = *reinterpret_cast<const float4*>(sk1 + poff + MN + off);
+                s1[0] = b.x; s1[1] = b.y; s1[2] = b.z; s1[3] = b.w;
+            }
+        }
+        if (own) {
+            // ---- rho_bar: -<Dvb, D x_k> ----
+            float dx0[4], dx1[4];
+            if (last_k) {
+                const float* xp = xK + (size_t)plane * MN;
+                const float4 xc = *reinterpret_cast<const float4*>(xp + off);
+                const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
+                const float xl = xp[(size_t)((j0 + t) & (N - 1)) * M + ((i - 1) & (M - 1))];
+                dx0[0] = xc.x - xq.x; dx0[1] = xc.y - xq.y; dx0[2] = xc.z - xq.z; dx0[3] = xc.w - xq.w;
+                dx1[0] = xc.x - xl; dx1[1] = xc.y - xc.x; dx1[2] = xc.z - xc.y; dx1[3] = xc.w - xc.z;
+            } else {
+                const float4 a = *reinterpret_cast<const float4*>(sk + poff + off);
+                const float4 b = *reinterpret_cast<const float4*>(sk + poff + MN + off);
+                const float a4[4] = {a.x, a.y, a.z, a.w}, b4[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    dx0[q] = a4[q] - fminf(fmaxf(s0[q], -tau), tau);
+                    dx1[q] = b4[q] - fminf(fmaxf(s1[q], -tau), tau);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rho_acc -= dv0[q] * dx0[q] + dv1[q] * dx1[q];
+            // ---- Vsum += vbar ----
+            float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
+            float4 acc = *vs;
+            acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
+            *vs = acc;
+        }
+        if (!first_k) {
+            float sb0[4] = {0, 0, 0, 0}, sb1[4] = {0, 0, 0, 0};   // sbar_k
+            if (sb_in) {
+                const float4 a = *reinterpret_cast<const float4*>(sb_in + poff + off);
+                sb0[0] = a.x; sb0[1] = a.y; sb0[2] = a.z; sb0[3] = a.w;
+                if (own) {
+                    const float4 b = *reinterpret_cast<const float4*>(sb_in + poff + MN + off);
+                    sb1[0] = b.x; sb1[1] = b.y; sb1[2] = b.z; sb1[3] = b.w;
+                }
+            }
+            float n0[4], n1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float wb = rho * dv0[q];
+                const bool m = fabsf(s0[q]) > tau;
+                n0[q] = m ? wb : sb0[q] - wb;
+                if (own) {
+                    rho_acc += phi_f(s0[q], tau) * dv0[q];
+                    if (m) tau_acc += sgnf(s0[q]) * (sb0[q] - 2.0f * wb);
+                }
+            }
+            *reinterpret_cast<float4*>(SB0 + t * M + i) = make_float4(n0[0], n0[1], n0[2], n0[3]);
+            if (own) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float wb = rho * dv1[q];
+                    const bool m = fabsf(s1[q]) > tau;
+                    n1[q] = m ? wb : sb1[q] - wb;
+                    rho_acc += phi_f(s1[q], tau) * dv1[q];
+                    if (m) tau_acc += sgnf(s1[q]) * (sb1[q] - 2.0f * wb);
+                }
+                *reinterpret_cast<float4*>(SB1 + t * M + i) = make_float4(n1[0], n1[1], n1[2], n1[3]);
+                *reinterpret_cast<float4*>(sb_out + poff + off) = make_float4(n0[0], n0[1], n0[2], n0[3]);
+                *reinterpret_cast<float4*>(sb_out + poff + MN + off) = make_float4(n1[0], n1[1], n1[2], n1[3]);
+            }
+        }
+    }
+    block_sum2(rho_acc, tau_acc, part + 2 * ((size_t)plane * gridDim.x + blockIdx.x), red);
+    if (first_k) return;   // k = 1: no g_0 (block-uniform)
+    __syncthreads();
+    // ---- g_{k-1} = D^T sbar_{k-1}, fed straight into the forward pass 0 along dim 1 ----
+    float2* F0 = const_cast<float2*>(reinterpret_cast<const float2*>(vb));   // vbar dead now
+    for (int idx = tid; idx < T * QF; idx += kThreads) {
+        const int f = idx / QF, j = idx - f * QF;
+        float2 v[RF];
+#pragma unroll
+        for (int r = 0; r < RF; ++r) {
+            const int n = j + r * QF;
+            const float2 a = *reinterpret_cast<const float2*>(SB0 + f * M + 2 * n);
+            const float2 b = *reinterpret_cast<const float2*>(SB0 + (f + 1) * M + 2 * n);
+            const float2 c = *reinterpret_cast<const float2*>(SB1 + f * M + 2 * n);
+            const float cn = SB1[f * M + ((2 * n + 2) & (M - 1))];
+            v[r].x = (a.x - b.x) + (c.x - c.y);
+            v[r].y = (a.y - b.y) + (c.y - cn);
+        }
+        fly_core<L, RF, 0, false, 2>(v, j, tw);
+        const int o = out_base<L, RF, 0>(j);
+#pragma unroll
+        for (int r = 0; r < RF; ++r) F0[f * L + o + r] = v[r];
+    }
+    __syncthreads();
+    float2* Z;
+    if constexpr (P == 1) {
+        Z = F0;
+    } else if constexpr (P == 2) {
+        float2* Zb = reinterpret_cast<float2*>(SB0);
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{Zb, L});
+        __syncthreads();
+        Z = Zb;
+    } else {
+        float2* Zb = reinterpret_cast<float2*>(SB0);
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{Zb, L});
+        __syncthreads();
+        plan_pass<L, 2, true, false, 2>(T, tw, LdsIO{Zb, L}, LdsIO{F0, L});
+        __syncthreads();
+        Z = F0;
+    }
+    pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
+}
+
+// h_bar through H^T y: hb[b][a] = sum_planes sum_px Vsum[j][i] * y[j+b-padr][i+a-padd]  (one block per
+// (plane, line tile); per-tap partials, deterministic order).  Tile of TY lines, y halo in LDS.
+__global__ __launch_bounds__(kThreads) void hbar_corr_kernel(const float* __restrict__ vsum, const float* __restrict__ y,
+                                                             double* __restrict__ part, int M, int N, int kh, int kw,
+                                                             int TY) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float* Vt = reinterpret_cast<float*>(smem_raw);        // TY lines
+    float* Yt = Vt + (size_t)TY * M;                        // TY + kw - 1 lines
+    const int plane = blockIdx.y;
+    const int j0 = blockIdx.x * TY;
+    const int padd = (kh - 1) / 2, padr = (kw - 1) / 2;
+    const size_t MN = (size_t)M * N;
+    const float* vp = vsum + (size_t)plane * MN;
+    const float* yp = y + (size_t)plane * MN;
+    for (int idx = threadIdx.x; idx < TY * M; idx += blockDim.x) Vt[idx] = vp[(size_t)j0 * M + idx];
+    for (int idx = threadIdx.x; idx < (TY + kw - 1) * M; idx += blockDim.x) {
+        const int r = idx / M, i = idx - r * M;
+        Yt[idx] = yp[(size_t)((j0 - padr + r) & (N - 1)) * M + i];
+    }
+    __syncthreads();
+    const int ntaps = kh * kw;
+    double* out = part + ((size_t)plane * gridDim.x + blockIdx.x) * ntaps;
+    // one wave per tap at a time: lanes stride over the tile's pixels
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int tap = wave; tap < ntaps; tap += nw) {
+        const int b = tap / kh, a = tap - b * kh;
+        float acc = 0.0f;
+        for (int p = lane; p < TY * M; p += 64) {
+            const int t = p / M, i = p - t * M;
+            acc += Vt[p] * Yt[(t + b) * M + ((i + a - padd) & (M - 1))];
+        }
+        double d = acc;
+        for (int off = 32; off > 0; off >>= 1) d += __shfl_down(d, off);
+        if (lane == 0) out[tap] = d;
+    }
+}
+
+// Sum column c (= blockIdx.x) of an n x w row-major matrix of per-block partials, in a fixed order.
+__global__ __launch_bounds__(kThreads) void reduce_cols_kernel(const double* __restrict__ part,
+                                                               double* __restrict__ out, int n, int w) {
+    __shared__ double red[kThreads];
+    const int c = blockIdx.x;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[(size_t)i * w + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = red[0];
+}
+
+// h_bar through A (needs Q): hbA[b][a] = -(1/MN) sum_{kj, k=0..L} w_k C^2 Q d|Sigma|^2/dh[b][a],
+// d|Sigma|^2/dh = 2 Re(conj(Sigma) e^{-2 pi i (a k/M + b kj/N)}); Sigma rebuilt in fp64.  One block per tap.
+__global__ __launch_bounds__(kThreads) void hbarA_kernel(const double* __restrict__ Q, const float* __restrict__ Ct,
+                                                         const double2* __restrict__ SigT, int kh, int M, int N,
+                                                         double* __restrict__ out) {
+    __shared__ double red[kThreads / 64];
+    const int tap = blockIdx.x;
+    const int b = tap / kh, a = tap - b * kh;
+    const int L = M / 2, H = L + 1;
+    double acc = 0.0;
+    for (int q = threadIdx.x; q < H * N; q += blockDim.x) {
+        const int kj = q / H, k = q - kj * H;
+        double s, c;
+        sincospi(-2.0 * ((double)((a * k) % M) / M + (double)((b * kj) % N) / N), &s, &c);
+        const double2 S = SigT[q];
+        const double dS = 2.0 * (S.x * c + S.y * s);    // 2 Re(conj(Sigma) e^{-i th})
+        const double Cm = (double)Ct[q] * (double)M * (double)N;   // Ct holds C/(MN)
+        const double wk = (k == 0 || k == L) ? 1.0 : 2.0;
+        acc += wk * Cm * Cm * Q[q] * dS;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) red[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sum = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) sum += red[i];
+        out[tap] = -sum / ((double)M * (double)N);
+    }
+}
+
+// Q[q] = sum over planes of Qp[p][q] (fixed order, fp64 result)
+__global__ void reduce_planes_kernel(const float* __restrict__ Qp, double* __restrict__ Q, int planes, int n) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int p = 0; p < planes; ++p) s += Qp[(size_t)p * n + q];
+        Q[q] = s;
+    }
+}
+
+// Final assembly of the scalar / PSF gradients into the caller's fp32 outputs.
+__global__ void grads_final_kernel(const double* __restrict__ rt, const double* __restrict__ hb_corr,
+                                   const double* __restrict__ hb_A, int ntaps, float lam, float rho,
+                                   float* __restrict__ lam_bar, float* __restrict__ rho_bar, float* __restrict__ h_bar) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        const double tau_bar = rt[1];
+        if (lam_bar) *lam_bar = (float)(tau_bar / rho);
+        if (rho_bar) *rho_bar = (float)(rt[0] - tau_bar * lam / ((double)rho * rho));
+    }
+    if (h_bar && t < ntaps) h_bar[t] = (float)(hb_corr[t] + (hb_A ? hb_A[t] : 0.0));
+}
+
+}  // namespace admm

@@ -19,6 +19,7 @@
 
 #include "../../include/admm_deconv.h"
 #include "admm_kernels.hip"
+#include "admm_backward.hip"
 
 namespace {
 
@@ -237,21 +238,31 @@ int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* s
     return -1;
 }
 
-int launch_column(int N, bool cplx, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
-                  const float* C, const float2* G, const float2* twN, int L, int KB, float cs) {
-#define X(v)                                                                                 \
-    if (N == v) {                                                                            \
-        if (cplx) {                                                                          \
-            set_lds(column_kernel<v, true>, lds);                                            \
-            column_kernel<v, true><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs);  \
-        } else {                                                                             \
-            set_lds(column_kernel<v, false>, lds);                                           \
-            column_kernel<v, false><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs); \
-        }                                                                                    \
-        return 0;                                                                            \
+template <int MUL, bool SAVE, bool ACCQ>
+int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst, const float* C,
+                    const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, float* Qp) {
+#define X(v)                                                                                                   \
+    if (N == v) {                                                                                              \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ>, lds);                                                       \
+        column_kernel<v, MUL, SAVE, ACCQ><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \
+        return 0;                                                                                              \
     }
     ADMM_N_CASES(X)
 #undef X
+    return -1;
+}
+
+// mode: 0 = x-update C, 1 = conj(Sigma_c) (H^T), 2 = Sigma_c (H), 3 = C + save spectrum, 4 = C + accumulate Q
+int launch_column(int N, int mode, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
+                  const float* C, const float2* G, const float2* twN, int L, int KB, float cs,
+                  float2* vsave = nullptr, float* Qp = nullptr) {
+    switch (mode) {
+        case 0: return launch_column_t<0, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+        case 1: return launch_column_t<1, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+        case 2: return launch_column_t<2, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+        case 3: return launch_column_t<0, true, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+        case 4: return launch_column_t<0, false, true>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+    }
     return -1;
 }
 
@@ -284,31 +295,25 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
     return ADMM_OK;
 }
 
-int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
-                         float lambda, float rho, int iso, int maxit, void* workspace, size_t workspace_bytes,
-                         void* stream) {
-    if (h == nullptr) kh = kw = 0;
-    int rc = check_shape(M, N, P, B, kh, kw, iso);
-    if (rc) return rc;
-    if (!y || !x_out) return fail(ADMM_E_INVALID, "y and x_out must be device pointers");
-    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
-    if (!std::isfinite(lambda) || !std::isfinite(rho)) return fail(ADMM_E_INVALID, "lambda and rho must be finite");
-    const size_t planes = (size_t)P * B;
-    const Layout lay = make_layout(M, N, planes, kh > 0, iso != 0);
-    if (!workspace || workspace_bytes < lay.total)
-        return fail(ADMM_E_WORKSPACE, "workspace too small: need %zu bytes, got %zu", lay.total, workspace_bytes);
-    if ((reinterpret_cast<uintptr_t>(workspace) & 255) != 0)
-        return fail(ADMM_E_WORKSPACE, "workspace must be 256-byte aligned");
-    if ((reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(x_out) & 15))
-        return fail(ADMM_E_INVALID, "y and x_out must be 16-byte aligned");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+}  // extern "C"
+
+namespace {
+
+// Trajectory recorded by the forward for the backward (all optional).
+struct Traj {
+    float* s = nullptr;      // (K-1) x planes x 2 x M x N : s_k for k = 1..K-1
+    float2* v = nullptr;     // K x planes x N x M/2        : forward dim-2 spectra (h_bar only)
+    double2* sig = nullptr;  // (M/2+1) x N                 : top-left PSF spectrum (h_bar only)
+};
+
+// Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
+// Returns the Launcher's status; `ln` keeps the events for the profiler.
+int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
+                int kw, float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                const Traj& tr) {
+    hipStream_t s = ln.s;
+    int rc = ADMM_OK;
     const size_t MN = (size_t)M * N;
-    if (maxit == 0) {
-        hipError_t e = hipMemsetAsync(x_out, 0, planes * MN * 4, s);
-        if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
-        return ADMM_OK;
-    }
-    unsigned char* ws = static_cast<unsigned char*>(workspace);
     float2* twM = reinterpret_cast<float2*>(ws + lay.twM);
     float2* twN = reinterpret_cast<float2*>(ws + lay.twN);
     float* Ct = reinterpret_cast<float*>(ws + lay.C);
@@ -319,81 +324,333 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
     float2* spec1 = reinterpret_cast<float2*>(ws + lay.spec1);
     const int L = M / 2;
     const float tau = lambda / rho;   // ops.jl:20
+    double2* SigT = tr.sig;
 
-    Launcher ln{s, g_prof.on, {}};
     rc = ln.run(ADMM_K_SETUP, [&] {
         const size_t lds = (size_t)(M + N) * 16;
         const int nb = (int)(((size_t)(L + 1) * N + kThreads - 1) / kThreads);
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
         hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Ct, Gt, h, kh, kw, M,
-                           N, rho);
+                           N, rho, SigT);
     });
     if (rc) return rc;
+    if (maxit == 0) {
+        hipError_t e = hipMemsetAsync(x_out, 0, planes * MN * 4, s);
+        if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+        return ADMM_OK;
+    }
 
     const int T = line_T(M, N);
     const int KB = column_KB(M, N);
     const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
     float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
-    const int kMaxY = 65535;
-    for (size_t p0 = 0; p0 < planes; p0 += kMaxY) {
-        const int np = (int)((planes - p0) < (size_t)kMaxY ? (planes - p0) : (size_t)kMaxY);
-        const float* yp = y + p0 * MN;
-        float* htyp = hty + p0 * MN;
-        float2* sp0 = spec0 + p0 * N * L;
-        float2* sp1 = spec1 + p0 * N * L;
-        float* sa = sbuf[0] + p0 * 2 * MN;
-        float* sb = sbuf[1] + p0 * 2 * MN;
-        float* xp = x_out + p0 * MN;
-        const dim3 gl(N / T, np), gc(L / KB, np);
-        // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
-        rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, yp, sp0, twM, N); });
+    const size_t np = planes;
+    const dim3 gl(N / T, (unsigned)np), gc(L / KB, (unsigned)np);
+    // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
+    rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
+    if (rc) return rc;
+    const float2* first = spec0;
+    float cs1 = 1.0f;
+    if (kh > 0) {
+        rc = ln.run(ADMM_K_PREP, [&] { launch_column(N, 1, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f); });
         if (rc) return rc;
-        const float2* first = sp0;
-        float cs1 = 1.0f;
-        if (kh > 0) {
-            rc = ln.run(ADMM_K_PREP, [&] { launch_column(N, true, gc, clds, s, sp0, sp1, Ct, Gt, twN, L, KB, 1.0f); });
-            if (rc) return rc;
-            rc = ln.run(ADMM_K_PREP, [&] { launch_line_inv(L, T, gl, flds, s, sp1, htyp, twM, N); });
-            if (rc) return rc;
-            first = sp1;          // = F_dim1(H^T y) / M
-            cs1 = (float)M;
-        }
-        for (int it = 1; it <= maxit; ++it) {
-            rc = ln.run(ADMM_K_COLUMN, [&] {
-                launch_column(N, false, gc, clds, s, it == 1 ? first : sp0, sp1, Ct, Gt, twN, L, KB,
-                              it == 1 ? cs1 : 1.0f);
+        rc = ln.run(ADMM_K_PREP, [&] { launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
+        if (rc) return rc;
+        first = spec1;          // = F_dim1(H^T y) / M
+        cs1 = (float)M;
+    }
+    const size_t sstride = np * 2 * MN;   // one trajectory slot of s
+    for (int it = 1; it <= maxit; ++it) {
+        float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * np * N * L : nullptr;
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            launch_column(N, vsave ? 3 : 0, gc, clds, s, it == 1 ? first : spec0, spec1, Ct, Gt, twN, L, KB,
+                          it == 1 ? cs1 : 1.0f, vsave);
+        });
+        if (rc) return rc;
+        if (it < maxit && !iso) {
+            float* so;
+            float* sn;
+            if (tr.s) {
+                so = it >= 2 ? tr.s + (size_t)(it - 2) * sstride : sbuf[0];
+                sn = tr.s + (size_t)(it - 1) * sstride;
+            } else {
+                so = (it & 1) ? sbuf[1] : sbuf[0];   // iteration 1 reads nothing (s_zero)
+                sn = (it & 1) ? sbuf[0] : sbuf[1];
+            }
+            rc = ln.run(ADMM_K_LINE, [&] {
+                launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, hty, twM, N, tau, rho, it == 1 ? 1 : 0);
+            });
+        } else if (it < maxit) {
+            // isotropic: s is written in place (no halo reads of s in ISO_A)
+            float* sa = sbuf[0];
+            const int ng = (int)((np + kIsoGroup - 1) / kIsoGroup);
+            rc = ln.run(ADMM_K_LINE, [&] {
+                launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, sa, sa, fmap, part, twM, N, (int)np,
+                             kIsoGroup, it == 1 ? 1 : 0);
             });
             if (rc) return rc;
-            if (it < maxit && !iso) {
-                float* so = (it & 1) ? sb : sa;   // iteration 1 reads nothing (s_zero)
-                float* sn = (it & 1) ? sa : sb;
-                rc = ln.run(ADMM_K_LINE, [&] {
-                    launch_line(L, T, gl, llds, s, sp1, sp0, so, sn, htyp, twM, N, tau, rho, it == 1 ? 1 : 0);
-                });
-            } else if (it < maxit) {
-                // isotropic: s is written in place (no halo reads of s in ISO_A)
-                const int ng = (np + kIsoGroup - 1) / kIsoGroup;
-                rc = ln.run(ADMM_K_LINE, [&] {
-                    launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, sp1, sa, sa, fmap, part, twM, N, np,
-                                 kIsoGroup, it == 1 ? 1 : 0);
-                });
-                if (rc) return rc;
-                rc = ln.run(ADMM_K_NORM, [&] {
-                    const int nb = (int)((MN + kThreads - 1) / kThreads);
-                    hipLaunchKernelGGL(admm::iso_r_kernel, dim3(nb < 2048 ? nb : 2048), dim3(kThreads), 0, s, part,
-                                       fmap, ng, MN, tau);
-                });
-                if (rc) return rc;
-                rc = ln.run(ADMM_K_LINE, [&] {
-                    launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sa, fmap, htyp, sp0, twM, N, rho);
-                });
-            } else {
-                rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, sp1, xp, twM, N); });
-            }
+            rc = ln.run(ADMM_K_NORM, [&] {
+                const int nb = (int)((MN + kThreads - 1) / kThreads);
+                hipLaunchKernelGGL(admm::iso_r_kernel, dim3(nb < 2048 ? nb : 2048), dim3(kThreads), 0, s, part,
+                                   fmap, ng, MN, tau);
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_LINE, [&] {
+                launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sa, fmap, hty, spec0, twM, N, rho);
+            });
+        } else {
+            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
+        }
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
+int check_common(const float* y, float* x, int maxit, float lambda, float rho) {
+    if (!y || !x) return fail(ADMM_E_INVALID, "y and x_out must be device pointers");
+    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
+    if (!std::isfinite(lambda) || !std::isfinite(rho)) return fail(ADMM_E_INVALID, "lambda and rho must be finite");
+    if ((reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(x) & 15))
+        return fail(ADMM_E_INVALID, "y and x_out must be 16-byte aligned");
+    return ADMM_OK;
+}
+
+int check_ws(void* workspace, size_t have, size_t need) {
+    if (!workspace || have < need) return fail(ADMM_E_WORKSPACE, "workspace too small: need %zu bytes, got %zu", need, have);
+    if ((reinterpret_cast<uintptr_t>(workspace) & 255) != 0) return fail(ADMM_E_WORKSPACE, "workspace must be 256-byte aligned");
+    return ADMM_OK;
+}
+
+// backward workspace = forward layout + trajectory + reverse-sweep buffers
+struct BwdLayout {
+    Layout f;
+    size_t traj_s, traj_v, sig, sbA, sbB, vsum, rpart, Qp, Q, hpart, hcorr, hA, rt, total;
+    int nblk_line, nblk_corr, TY;
+};
+
+BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h) {
+    BwdLayout b{};
+    b.f = make_layout(M, N, planes, kh > 0, false);
+    size_t off = b.f.total;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes);
+        return o;
+    };
+    const size_t MN = (size_t)M * N;
+    const int K = maxit < 1 ? 1 : maxit;
+    const int T = line_T(M, N);
+    const bool hq = want_h && kh > 0;
+    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * 2 * MN * 4);
+    b.traj_v = hq ? take((size_t)K * planes * MN * 4) : 0;
+    b.sig = hq ? take((size_t)(M / 2 + 1) * N * 16) : 0;
+    b.sbA = take(planes * 2 * MN * 4);
+    b.sbB = take(planes * 2 * MN * 4);
+    b.vsum = take(planes * MN * 4);
+    b.nblk_line = (int)(planes * (N / T));
+    b.rpart = take((size_t)K * b.nblk_line * 2 * 8);
+    b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 4) : 0;
+    b.Q = hq ? take((size_t)(M / 2 + 1) * N * 8) : 0;
+    b.TY = N < 8 ? N : 8;
+    b.nblk_corr = (int)(planes * (N / b.TY));
+    b.hpart = kh > 0 ? take((size_t)b.nblk_corr * kh * kw * 8) : 0;
+    b.hcorr = kh > 0 ? take((size_t)kh * kw * 8) : 0;
+    b.hA = hq ? take((size_t)kh * kw * 8) : 0;
+    b.rt = take(2 * 8);
+    b.total = off;
+    return b;
+}
+
+int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
+                    const float* sk, const float* xK, const float* sb_in, float* sb_out, float* vsum, float2* spec0,
+                    double* part, const float2* twM, int N, float tau, float rho, int first_k, int last_k) {
+#define X(l, t)                                                                                                \
+    if (L == l && T == t) {                                                                                    \
+        set_lds(line_adj_kernel<l, t>, lds);                                                                   \
+        line_adj_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, part, twM, \
+                                                        N, tau, rho, first_k, last_k);                        \
+        return 0;                                                                                              \
+    }
+    ADMM_LT_CASES(X)
+#undef X
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
+                         float lambda, float rho, int iso, int maxit, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    if (h == nullptr) kh = kw = 0;
+    int rc = check_shape(M, N, P, B, kh, kw, iso);
+    if (rc) return rc;
+    rc = check_common(y, x_out, maxit, lambda, rho);
+    if (rc) return rc;
+    const size_t planes = (size_t)P * B;
+    if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
+    const Layout lay = make_layout(M, N, planes, kh > 0, iso != 0);
+    rc = check_ws(workspace, workspace_bytes, lay.total);
+    if (rc) return rc;
+    Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
+    rc = run_forward(ln, y, x_out, M, N, planes, h, kh, kw, lambda, rho, iso, maxit,
+                     static_cast<unsigned char*>(workspace), lay, Traj{});
+    int rc2 = ln.finish();
+    return rc ? rc : rc2;
+}
+
+int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, int want_hbar,
+                                      size_t* out_bytes) {
+    if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
+    int rc = check_shape(M, N, P, B, kh, kw, iso);
+    if (rc) return rc;
+    if (iso) return fail(ADMM_E_UNSUPPORTED, "backward of the isotropic (BT) prox is not in this build yet");
+    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
+    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0).total;
+    return ADMM_OK;
+}
+
+int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                          float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw, float lambda,
+                          float rho, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
+                          void* stream) {
+    if (h == nullptr) kh = kw = 0;
+    int rc = check_shape(M, N, P, B, kh, kw, iso);
+    if (rc) return rc;
+    if (iso) return fail(ADMM_E_UNSUPPORTED, "backward of the isotropic (BT) prox is not in this build yet");
+    rc = check_common(y, y_bar, maxit, lambda, rho);
+    if (rc) return rc;
+    if (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)) return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
+    const size_t planes = (size_t)P * B;
+    if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
+    const bool want_h = h_bar != nullptr && kh > 0;
+    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h);
+    rc = check_ws(workspace, workspace_bytes, bl.total);
+    if (rc) return rc;
+    unsigned char* ws = static_cast<unsigned char*>(workspace);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    Launcher ln{s, g_prof.on, {}};
+    const size_t MN = (size_t)M * N;
+    const int L = M / 2;
+    const int T = line_T(M, N);
+    const int KB = column_KB(M, N);
+    const float tau = lambda / rho;
+    const int K = maxit;
+    if (!x_out || (reinterpret_cast<uintptr_t>(x_out) & 15))
+        return fail(ADMM_E_INVALID, "x_out (forward output of the recomputed solve) must be a 16-byte aligned device pointer");
+    float* xK = x_out;
+    hipError_t e;
+#define HIPCHK(call)                                                                           \
+    do {                                                                                       \
+        e = (call);                                                                            \
+        if (e != hipSuccess) return fail(ADMM_E_HIP, "%s: %s", #call, hipGetErrorString(e));   \
+    } while (0)
+    if (K == 0) {
+        HIPCHK(hipMemsetAsync(y_bar, 0, planes * MN * 4, s));
+        if (h_bar && kh > 0) HIPCHK(hipMemsetAsync(h_bar, 0, (size_t)kh * kw * 4, s));
+        if (lambda_bar) HIPCHK(hipMemsetAsync(lambda_bar, 0, 4, s));
+        if (rho_bar) HIPCHK(hipMemsetAsync(rho_bar, 0, 4, s));
+        if (x_out) HIPCHK(hipMemsetAsync(x_out, 0, planes * MN * 4, s));
+        return ln.finish();
+    }
+    // ---- forward with trajectory ----
+    Traj tr;
+    tr.s = reinterpret_cast<float*>(ws + bl.traj_s);
+    tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
+    tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
+    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, 0, K, ws, bl.f, tr);
+    if (rc) return rc;
+    // ---- reverse sweep ----
+    float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + bl.f.twN);
+    float* Ct = reinterpret_cast<float*>(ws + bl.f.C);
+    float2* Gt = kh > 0 ? reinterpret_cast<float2*>(ws + bl.f.G) : nullptr;
+    float2* specA = reinterpret_cast<float2*>(ws + bl.f.spec0);
+    float2* specB = reinterpret_cast<float2*>(ws + bl.f.spec1);
+    float* sb[2] = {reinterpret_cast<float*>(ws + bl.sbA), reinterpret_cast<float*>(ws + bl.sbB)};
+    float* vsum = reinterpret_cast<float*>(ws + bl.vsum);
+    double* rpart = reinterpret_cast<double*>(ws + bl.rpart);
+    float* Qp = want_h ? reinterpret_cast<float*>(ws + bl.Qp) : nullptr;
+    const size_t sstride = planes * 2 * MN;
+    const size_t clds = column_lds(N, KB), flds = fwdinv_lds(M, T);
+    const size_t alds = line_lds(M, T) + 8 * 16;
+    const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
+    HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
+    if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
+    rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
+    if (rc) return rc;
+    for (int k = K; k >= 1; --k) {
+        float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * L : nullptr;
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
+        });
+        if (rc) return rc;
+        const float* sk1 = k >= 2 ? tr.s + (size_t)(k - 2) * sstride : nullptr;
+        const float* skk = k < K ? tr.s + (size_t)(k - 1) * sstride : nullptr;
+        const float* sbi = k < K ? sb[k & 1] : nullptr;
+        float* sbo = sb[(k & 1) ^ 1];
+        double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
+        rc = ln.run(ADMM_K_LINE, [&] {
+            launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
+                            k == 1 ? 1 : 0, k == K ? 1 : 0);
+        });
+        if (rc) return rc;
+    }
+    // ---- assembly ----
+    double* rt = reinterpret_cast<double*>(ws + bl.rt);
+    rc = ln.run(ADMM_K_FINAL, [&] {
+        hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(2), dim3(kThreads), 0, s, rpart, rt, K * bl.nblk_line, 2);
+    });
+    if (rc) return rc;
+    double* hcorr = kh > 0 ? reinterpret_cast<double*>(ws + bl.hcorr) : nullptr;
+    double* hA = want_h ? reinterpret_cast<double*>(ws + bl.hA) : nullptr;
+    if (kh > 0) {
+        // y_bar = H vsum  (centred circular convolution, spectrally)
+        rc = ln.run(ADMM_K_FINAL, [&] { launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_FINAL, [&] { launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, specB, y_bar, twM, N); });
+        if (rc) return rc;
+        if (h_bar) {
+            double* hpart = reinterpret_cast<double*>(ws + bl.hpart);
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                const size_t lds = (size_t)(2 * bl.TY + kw - 1) * M * 4;
+                set_lds(admm::hbar_corr_kernel, lds);
+                hipLaunchKernelGGL(admm::hbar_corr_kernel, dim3(N / bl.TY, (unsigned)planes), dim3(kThreads), lds, s,
+                                   vsum, y, hpart, M, N, kh, kw, bl.TY);
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(kh * kw), dim3(kThreads), 0, s, hpart, hcorr,
+                                   bl.nblk_corr, kh * kw);
+            });
+            if (rc) return rc;
+            double* Q = reinterpret_cast<double*>(ws + bl.Q);
+            const int nq = (L + 1) * N;
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(admm::reduce_planes_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, Qp, Q,
+                                   (int)planes, nq);
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(admm::hbarA_kernel, dim3(kh * kw), dim3(kThreads), 0, s, Q, Ct, tr.sig, kh, M, N,
+                                   hA);
+            });
             if (rc) return rc;
         }
+    } else {
+        HIPCHK(hipMemcpyAsync(y_bar, vsum, planes * MN * 4, hipMemcpyDeviceToDevice, s));
     }
+    rc = ln.run(ADMM_K_FINAL, [&] {
+        const int nt = kh * kw > 1 ? kh * kw : 1;
+        hipLaunchKernelGGL(admm::grads_final_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, rt, hcorr, hA, kh * kw,
+                           lambda, rho, lambda_bar, rho_bar, (h_bar && kh > 0) ? h_bar : nullptr);
+    });
+    if (rc) return rc;
+#undef HIPCHK
     return ln.finish();
 }
 

@@ -42,7 +42,7 @@ constexpr int kThreads = 256;
 __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ twM, float2* __restrict__ twN,
                                                          float* __restrict__ Ct, float2* __restrict__ Gt,
                                                          const float* __restrict__ h, int kh, int kw, int M,
-                                                         int N, float rho) {
+                                                         int N, float rho, double2* __restrict__ SigT) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     double2* tM = reinterpret_cast<double2*>(smem_raw);  // exp(-2 pi i t / M)
     double2* tN = tM + M;                                // exp(-2 pi i t / N)
@@ -85,6 +85,7 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
                 im += gr * eb.y + gi * eb.x;
             }
             s2 = re * re + im * im;
+            if (SigT) SigT[q] = make_double2(re, im);   // top-left PSF spectrum (backward h_bar)
             // centred spectrum: Sigma_c = Sigma * exp(+2 pi i (padd k/M + padr kj/N)); store conj / (MN)
             const double2 pa = tM[(padd * k) & (M - 1)];
             const double2 pb = tN[(padr * kj) & (N - 1)];
@@ -213,14 +214,19 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 // first pass touch the same points in the same thread: they run back to back in registers with the
 // multiply between (one LDS round trip saved).  One LDS buffer, in-place passes (read, barrier,
 // write); requires KB * NN / R <= blockDim for every radix R of the plan (host guarantees).
-//   CPLX = false: real multiplier Ct (the ADMM x-update), scaled by cs
-//   CPLX = true : complex multiplier Gt (H^T y setup)
+//   MUL = 0: real multiplier Ct (the ADMM x-update / its adjoint A^-1), scaled by cs
+//   MUL = 1: complex multiplier Gt = conj(Sigma_c)/(MN)   (H^T y setup)
+//   MUL = 2: conj(Gt) = Sigma_c/(MN)                       (y_bar = H vbar_sum in the backward)
+//   SAVE   : also store the forward dim-2 spectrum (before the multiply) to vsave (trajectory for h_bar)
+//   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar)
 // ----------------------------------------------------------------------------------------------
-template <int NN, bool CPLX>
+template <int NN, int MUL, bool SAVE, bool ACCQ>
 __global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, float2* dst,
                                                           const float* __restrict__ Ct,
                                                           const float2* __restrict__ Gt,
-                                                          const float2* __restrict__ twN, int L, int KB, float cs) {
+                                                          const float2* __restrict__ twN, int L, int KB, float cs,
+                                                          float2* __restrict__ vsave, float* __restrict__ Qp) {
+    constexpr bool CPLX = MUL != 0;
     constexpr int FS = NN + 1;  // per-transform LDS stride (odd: conflict-free slot-major stores)
     constexpr int P = Plan<NN>::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -301,13 +307,43 @@ __global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, flo
         __syncthreads();
         if (act) {
             const int s = k0 + f;
+            if constexpr (SAVE) {
+                float2* vs = vsave + (size_t)plane * NN * L + k0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) vs[(size_t)(j + r * Q) * L + f] = cscale(v[r], cs);
+            }
+            if constexpr (ACCQ) {
+                const float2* vs = vsave + (size_t)plane * NN * L;
+                float* qp = Qp + (size_t)plane * NN * H;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int kj = j + r * Q;
+                    const float2 gv = v[r];
+                    const float2 vv = vs[(size_t)kj * L + s];
+                    if (mirror && f == 0) {
+                        // separate the packed pair: A = (Z + conj Z(-kj))/2, B = (Z - conj Z(-kj))/(2i)
+                        const int km = (NN - kj) & (NN - 1);
+                        const float2 gm = cconj(S0[km]);
+                        const float2 vm = cconj(vs[(size_t)km * L]);
+                        const float2 ga = cscale(cadd(gv, gm), 0.5f), va = cscale(cadd(vv, vm), 0.5f);
+                        const float2 gd = csub(gv, gm), vd = csub(vv, vm);
+                        const float2 gb = make_float2(0.5f * gd.y, -0.5f * gd.x);
+                        const float2 vb = make_float2(0.5f * vd.y, -0.5f * vd.x);
+                        qp[(size_t)kj * H] += ga.x * va.x + ga.y * va.y;
+                        qp[(size_t)kj * H + L] += gb.x * vb.x + gb.y * vb.y;
+                    } else {
+                        qp[(size_t)kj * H + s] += gv.x * vv.x + gv.y * vv.y;
+                    }
+                }
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int kj = j + r * Q;
                 if (mirror && f == 0) {
                     const float2 zm = cconj(S0[(NN - kj) & (NN - 1)]);
                     if constexpr (CPLX) {
-                        const float2 m0 = Gt[(size_t)kj * H], mL = Gt[(size_t)kj * H + L];
+                        float2 m0 = Gt[(size_t)kj * H], mL = Gt[(size_t)kj * H + L];
+                        if constexpr (MUL == 2) { m0 = cconj(m0); mL = cconj(mL); }
                         const float2 a = cscale(cadd(m0, mL), 0.5f), b = cscale(csub(m0, mL), 0.5f);
                         v[r] = cadd(cmul(a, v[r]), cmul(b, zm));
                     } else {
@@ -315,7 +351,9 @@ __global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, flo
                         v[r] = cadd(cscale(v[r], 0.5f * cs * (c0 + cL)), cscale(zm, 0.5f * cs * (c0 - cL)));
                     }
                 } else {
-                    if constexpr (CPLX) {
+                    if constexpr (MUL == 2) {
+                        v[r] = cmul(v[r], cconj(Gt[(size_t)kj * H + s]));
+                    } else if constexpr (CPLX) {
                         v[r] = cmul(v[r], Gt[(size_t)kj * H + s]);
                     } else {
                         v[r] = cscale(v[r], cs * Ct[(size_t)kj * H + s]);

@@ -21,7 +21,7 @@
  *  - Return value: 0 on success, a negative ADMM_E* code otherwise; admm_last_error() gives a
  *    thread-local message for the last failing call.
  *  - Supported shapes (this build): M, N powers of two with 4 <= M <= 1024, 2 <= N <= 1024;
- *    kh <= M, kw <= N, kh*kw <= 4096.  Other shapes return ADMM_E_UNSUPPORTED (the reference accepts any
+ *    kh <= M, kw <= N.  Other shapes return ADMM_E_UNSUPPORTED (the reference accepts any
  *    M x N through FFTW/CUFFT; non-power-of-two sizes are a listed next step).
  */
 #ifndef ADMM_DECONV_H
@@ -73,6 +73,20 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
 int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B,
                          const float* h, int kh, int kw, float lambda, float rho, int iso,
                          int maxit, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Adjoint of admm_tvd_forward_f32 (the Zygote reverse pass through the K unrolled iterations that
+ * the reference's training uses, src/train.jl:51 with src/ops/ops.jl:84-92; BASELINE config c5).
+ * Recomputes the forward (writing x to x_out) while recording one state tensor per iteration, then
+ * runs the reverse sweep.  Given x_bar = dL/dx it writes
+ *   y_bar (device, shape of y)   h_bar (device, kw*kh floats; NULL = not needed, cheaper)
+ *   lambda_bar, rho_bar (device, 1 float each; NULL = not needed)
+ * Anisotropic prox only in this build (iso != 0 returns ADMM_E_UNSUPPORTED).  Deterministic. */
+int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso, int maxit,
+                                      int want_hbar, size_t* out_bytes);
+int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                          float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
+                          const float* h, int kh, int kw, float lambda, float rho, int iso, int maxit,
+                          float* x_out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises

@@ -1,0 +1,83 @@
+"""Differentiable CPU oracle (PyTorch, fp64) -- TEST INFRASTRUCTURE ONLY.
+
+A torch restatement of /root/reference/src/ops/ops.jl:17-96 (same operators as oracle_np.py's
+literal form: np.roll stencils, spatial H^T with the pad2 offsets, rfft/irfft over dims (1,2)),
+used as the gradient oracle for the adjoint (the reference gets its gradients
+from Zygote unrolling the loop, src/train.jl:51).  torch.autograd differentiates ST/BT exactly as
+Zygote's broadcast rules do away from the kinks (sign' = 0, max(., 0)' = step).
+Parity status: unpinned against Julia (see oracle_np.py); pinned against oracle_np by tests.
+
+Arrays are C layout (B, P, N, M) like the C ABI; the PSF is (kw, kh).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def _ht(y, h):
+    """H^T y (ops.jl:72-81): sum_{a,b} h[b,a] y[i+a-padd, j+b-padr]; y (..., N, M), h (kw, kh)."""
+    kw, kh = h.shape
+    padd, padr = (kh - 1) // 2, (kw - 1) // 2
+    out = torch.zeros_like(y)
+    for b in range(kw):
+        for a in range(kh):
+            out = out + h[b, a] * torch.roll(y, shifts=(-(b - padr), -(a - padd)), dims=(-2, -1))
+    return out
+
+
+def _make_C(M, N, rho, h):
+    """ops.jl:22-37; differentiable in rho and h.  Shape (N, M//2+1) (rfft over the last dim)."""
+    dev, dt = rho.device, rho.dtype
+    if h is None:
+        s2 = torch.ones((N, M // 2 + 1), dtype=dt, device=dev)
+    else:
+        kw, kh = h.shape
+        hh = torch.zeros((N, M), dtype=dt, device=dev)
+        hh = hh.index_put((torch.arange(kw).repeat_interleave(kh), torch.arange(kh).repeat(kw)), h.reshape(-1))
+        S = torch.fft.rfft2(hh)
+        s2 = S.real ** 2 + S.imag ** 2
+    k = torch.arange(M // 2 + 1, dtype=dt, device=dev)[None, :]
+    kj = torch.arange(N, dtype=dt, device=dev)[:, None]
+    lap = 4 * torch.sin(torch.pi * kj / N) ** 2 + 4 * torch.sin(torch.pi * k / M) ** 2
+    return 1.0 / (s2 + rho * lap)
+
+
+def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100):
+    """y: (B,P,N,M) float64 tensor; lam, rho: 0-d tensors; h: (kw,kh) tensor or None.  Returns x."""
+    B, P, N, M = y.shape
+    tau = lam / rho                                                   # ops.jl:20
+    C = _make_C(M, N, rho, h)
+    hty = y if h is None else _ht(y, h)
+    x = torch.zeros_like(y)
+    z1 = torch.zeros_like(y); z2 = torch.zeros_like(y)
+    u1 = torch.zeros_like(y); u2 = torch.zeros_like(y)
+    for _ in range(maxit):
+        w1, w2 = z1 - u1, z2 - u2
+        dtw = (w1 - torch.roll(w1, -1, dims=-2)) + (w2 - torch.roll(w2, -1, dims=-1))
+        x = torch.fft.irfft2(C * torch.fft.rfft2(hty + rho * dtw), s=(N, M))
+        d1 = x - torch.roll(x, 1, dims=-2)                             # x[i,j]-x[i,j-1]
+        d2 = x - torch.roll(x, 1, dims=-1)                             # x[i,j]-x[i-1,j]
+        s1, s2 = d1 + u1, d2 + u2
+        if isotropic:
+            nrm = torch.sqrt((s1 * s1 + s2 * s2).sum(dim=(0, 1), keepdim=True))
+            f = torch.clamp(1 - tau / nrm, min=0.0)
+            z1, z2 = f * s1, f * s2
+        else:
+            z1 = torch.sign(s1) * torch.clamp(torch.abs(s1) - tau, min=0.0)
+            z2 = torch.sign(s2) * torch.clamp(torch.abs(s2) - tau, min=0.0)
+        u1, u2 = u1 + d1 - z1, u2 + d2 - z2
+    return x
+
+
+def tvd_fft_grads(y, lam, rho, h, iso, maxit, xbar):
+    """fp64 autograd gradients of <xbar, x(y, lam, rho, h)>: returns (x, ybar, hbar, lambar, rhobar)."""
+    y = torch.as_tensor(y, dtype=torch.float64).clone().requires_grad_(True)
+    lam_t = torch.tensor(float(lam), dtype=torch.float64, requires_grad=True)
+    rho_t = torch.tensor(float(rho), dtype=torch.float64, requires_grad=True)
+    h_t = None
+    if h is not None and h.size:
+        h_t = torch.as_tensor(h, dtype=torch.float64).clone().requires_grad_(True)
+    x = tvd_fft_torch(y, lam_t, rho_t, h_t, iso, maxit)
+    (x * torch.as_tensor(xbar, dtype=torch.float64)).sum().backward()
+    return (x.detach().numpy(), y.grad.numpy(), None if h_t is None else h_t.grad.numpy(),
+            float(lam_t.grad) if lam_t.grad is not None else 0.0, float(rho_t.grad) if rho_t.grad is not None else 0.0)
