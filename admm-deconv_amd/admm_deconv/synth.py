@@ -79,6 +79,15 @@ def noise(g, n, sigma=0.01):
     return sigma * np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
 
 
+def make_clean(B, M, N, P=1, g0=0):
+    """The ground-truth images of make_batch (no blur, no noise), float32 (B,P,N,M)."""
+    out = np.empty((B, P, N, M), np.float32)
+    for b in range(B):
+        for p in range(P):
+            out[b, p] = ground_truth((g0 + b) * P + p, M, N).astype(np.float32)
+    return out
+
+
 def make_batch(B, M, N, psf_c, P=1, g0=0, sigma=0.01):
     """float32 array (B, P, N, M) of blurred noisy images with global indices g0..g0+B-1."""
     out = np.empty((B, P, N, M), np.float32)
@@ -98,5 +107,8 @@ CONFIGS = {
     "c2": dict(M=256, N=256, P=1, B=512, psf=(15, 2.5), K=25),
     "c3": dict(M=256, N=256, P=1, B=2048, psf=(15, 2.5), K=25),
     "c4": dict(M=512, N=512, P=3, B=256, psf=(15, 2.5), K=50),
+    # c5: the get_denoiser branch (src/nets/net_build.jl:113-128): 5 x ADMMDeconvF2((), 50, rho, relu1),
+    # batch 64 of 256x256 RGB (train_cfg.json im_shape), forward + adjoint
+    "c5": dict(M=256, N=256, P=3, B=64, psf=None, K=50),
 }
 LAMBDA, RHO = 0.0041, 0.021   # src/tests/admm_deconv_test.jl:76

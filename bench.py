@@ -65,12 +65,68 @@ def parse():
 
 
 def make_inputs(cfg, B, g0, distinct, dev):
-    psf = synth.gaussian_psf(*cfg["psf"])
+    psf = synth.gaussian_psf(*cfg["psf"]) if cfg["psf"] else None
     nd = min(B, distinct)
     base = synth.make_batch(nd, cfg["M"], cfg["N"], psf, P=cfg["P"], g0=g0)
     reps = (B + nd - 1) // nd
     y = np.concatenate([base] * reps)[:B]
-    return torch.from_numpy(np.ascontiguousarray(y)).to(dev), torch.from_numpy(psf).to(dev), psf, base
+    return (torch.from_numpy(np.ascontiguousarray(y)).to(dev), None if psf is None else torch.from_numpy(psf).to(dev),
+            psf, base)
+
+
+def bench_c5(args, dev):
+    """BASELINE c5: the denoiser branch of src/nets/net_build.jl:113-128 (5 x ADMMDeconvF2((), 50, rho, relu1)
+    in Parallel(chcat)), batch 64 of 256x256 RGB; one step = forward + MSE loss + backward through the HIP
+    adjoint + SGD update of the trainable lambda (the layers' trainable set, deconv_admm.jl:107)."""
+    from admm_deconv import layers
+    cfg = synth.CONFIGS["c5"]
+    M, N, P, B, K = cfg["M"], cfg["N"], cfg["P"], args.batch or cfg["B"], cfg["K"]
+    rng = np.random.default_rng(0)
+    branch = [layers.ADMMDeconvF2((), K, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.02, 0.2, 2.0, 4.0)]
+    for L in branch:
+        L.lam.requires_grad_(True)
+    nd = min(B, args.distinct)
+    noisy = synth.make_batch(nd, M, N, None, P=P, sigma=0.1)
+    clean = synth.make_clean(nd, M, N, P=P)
+    reps = (B + nd - 1) // nd
+    x = torch.from_numpy(np.concatenate([noisy] * reps)[:B]).to(dev)
+    target = torch.from_numpy(np.concatenate([clean] * reps)[:B]).to(dev).repeat(1, len(branch), 1, 1)
+
+    def step():
+        out = torch.cat([L(x) for L in branch], dim=1)        # chcat (dim 3 in Julia = channels)
+        loss = torch.mean((out - target) ** 2)
+        loss.backward()
+        with torch.no_grad():
+            for L in branch:
+                L.lam -= 1e-3 * L.lam.grad
+                L.lam.grad = None
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    step()
+    _lib.profile_enable(False)
+    kernels = {}
+    for cls, name in _lib.KERNEL_CLASSES.items():
+        ms, n = _lib.profile_get(cls)
+        if n:
+            kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
+    print(json.dumps({
+        "metric": "c5 ADMM denoiser-branch train step (fwd + adjoint) images/s", "value": round(B * args.steps / el, 2),
+        "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
+                               "MSE, backward through admm_tvd_backward_f32 (aniso)", "global_batch": B},
+        "kernels": kernels}))
 
 
 def cpu_baseline(cfg, psf, base, target_s):
@@ -112,6 +168,8 @@ def load_traffic(cfg_name, kernel):
 
 def main():
     args = parse()
+    if args.config == "c5":
+        return bench_c5(args, torch.device("cuda", 0))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
