@@ -1,0 +1,48 @@
+// devtest.hip -- device-level unit tests of building blocks (built as libadmm_devtest.so; used only by
+// tests/test_gpu_devtest.py, never by the product path).
+#include <hip/hip_runtime.h>
+
+#include "line_pair.hpp"
+
+namespace {
+
+// one block = 512 threads = 256 lines (lane pair per line)
+__global__ __launch_bounds__(512) void pair_fwd_kernel(const float* __restrict__ x, float2* __restrict__ spec) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 1);
+    const bool hb = threadIdx.x & 1;
+    const float2* row = reinterpret_cast<const float2*>(x + (size_t)r * 256) + (hb ? 1 : 0);
+    float2 S[64];
+#pragma unroll
+    for (int n = 0; n < 64; ++n) S[n] = row[2 * n];
+    admm::line_forward_pair(S, hb);
+    float2* out = spec + (size_t)r * 128 + (hb ? 64 : 0);
+#pragma unroll
+    for (int m = 0; m < 64; ++m) out[m] = S[m];
+}
+
+__global__ __launch_bounds__(512) void pair_inv_kernel(const float2* __restrict__ spec, float* __restrict__ x) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 1);
+    const bool hb = threadIdx.x & 1;
+    const float2* in = spec + (size_t)r * 128 + (hb ? 64 : 0);
+    float2 S[64];
+#pragma unroll
+    for (int m = 0; m < 64; ++m) S[m] = in[m];
+    admm::line_inverse_pair(S, hb);
+    float2* row = reinterpret_cast<float2*>(x + (size_t)r * 256) + (hb ? 1 : 0);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) row[2 * n] = S[n];
+}
+
+}  // namespace
+
+extern "C" {
+// rows must be a multiple of 256; device pointers; synchronous
+int devtest_pair_forward(const float* x, float* spec, int rows) {
+    pair_fwd_kernel<<<rows / 256, 512>>>(x, reinterpret_cast<float2*>(spec));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+int devtest_pair_inverse(const float* spec, float* x, int rows) {
+    pair_inv_kernel<<<rows / 256, 512>>>(reinterpret_cast<const float2*>(spec), x);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+}

@@ -1,0 +1,185 @@
+// line_pair.hpp -- register-resident dim-1 transforms of a 256-sample real line held by a LANE PAIR.
+//
+// Used by the fused per-plane kernel (plane_kernel.hip): lane 2r ("A", h = 0) and lane 2r+1 ("B",
+// h = 1) hold line r.  With the half-length complex signal z[n] = x[2n] + i x[2n+1] (n = 0..127):
+//   spatial  : lane A register n holds z[2n]   = (x[4n],   x[4n+1])     n = 0..63
+//              lane B register n holds z[2n+1] = (x[4n+2], x[4n+3])
+//   spectral : lane A register m holds X[m]    (m = 0..63; register 0 = packed (X[0], X[128]))
+//              lane B register m holds X[64+m]
+//   forward: 64-point FFT of each lane's samples (even / odd half of z), the radix-2 DIT combine
+//            across the pair (Z[k] = E + W128^k O on A, Z[k+64] = E - W128^k O on B), then the
+//            real-to-complex post-processing X[k] = (Z[k] + conj Z[128-k])/2 + W256^k (..)/(2i).
+//            The mirror of register m is the PARTNER's register 64-m (m = 1..63), so the post-
+//            processing runs in place on register pairs (m, 64-m) with two pair swaps each.
+//   inverse: the exact reverse.  Unnormalised both ways: inverse(forward(x)) = 256 x, the same
+//            convention as the 2-pass kernels (1/(MN) lives in the spectral tables).
+// Every register index is a compile-time constant (no scratch); the only cross-lane operation is the
+// pair swap, one DPP quad_perm [1,0,3,2] move per dword.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "fft_reg.hpp"
+
+namespace admm {
+
+#include "tw256.inc"
+
+// v * W256^E (forward, W256 = exp(-2 pi i/256)) or v * conj(W256^E) (inverse)
+template <int E, bool INV>
+__device__ __forceinline__ float2 w256(float2 v) {
+    constexpr int e = E & 255;
+    if constexpr (e == 0) {
+        return v;
+    } else if constexpr (e == 64) {
+        return rot<INV>(v);
+    } else if constexpr (e == 128) {
+        return make_float2(-v.x, -v.y);
+    } else if constexpr (e == 192) {
+        return rot<!INV>(v);
+    } else {
+        constexpr float c = kC256[e];
+        constexpr float s = INV ? kS256[e] : -kS256[e];
+        return make_float2(fmaf(v.x, c, -v.y * s), fmaf(v.x, s, v.y * c));
+    }
+}
+
+// exchange with the partner lane (lane ^ 1) -- DPP quad_perm [1,0,3,2]
+__device__ __forceinline__ float swapf(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float2 swap_pair(float2 v) { return make_float2(swapf(v.x), swapf(v.y)); }
+
+// ---- in-register 64-point FFT, natural order in and out: 64 = 4 (n1) x 16 (n2) -----------------
+//   X[k1 + 4 k2] = sum_{n2} W16^{n2 k2} W64^{n2 k1} sum_{n1} x[16 n1 + n2] W4^{n1 k1}
+template <bool INV, int N2>
+__device__ __forceinline__ void fft64_tw(float2 (&t)[16][4]) {
+    t[N2][1] = w256<4 * N2 * 1, INV>(t[N2][1]);
+    t[N2][2] = w256<4 * N2 * 2, INV>(t[N2][2]);
+    t[N2][3] = w256<4 * N2 * 3, INV>(t[N2][3]);
+    if constexpr (N2 + 1 < 16) fft64_tw<INV, N2 + 1>(t);
+}
+
+// The scheduling fences keep the machine scheduler from interleaving the stages: left free it hoists
+// work across them and needs ~260 VGPRs (spilling at 2 waves/SIMD); fenced it needs ~160.
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+template <bool INV>
+__device__ __forceinline__ void fft64_reg(float2 (&x)[64]) {
+    float2 t[16][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) {
+        t[n2][0] = x[n2]; t[n2][1] = x[16 + n2]; t[n2][2] = x[32 + n2]; t[n2][3] = x[48 + n2];
+        dft4<INV>(t[n2][0], t[n2][1], t[n2][2], t[n2][3]);
+    }
+    sched_fence();
+    fft64_tw<INV, 1>(t);
+    sched_fence();
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        float2 u[16];
+#pragma unroll
+        for (int n2 = 0; n2 < 16; ++n2) u[n2] = t[n2][k1];
+        dft<16, INV>(u);
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) x[k1 + 4 * k2] = u[k2];
+        sched_fence();
+    }
+}
+
+// forward DIT combine across the pair: A: Z[k] = E[k] + W128^k O[k], B: Z[k+64] = E[k] - W128^k O[k]
+template <int K>
+__device__ __forceinline__ void combine_fwd(float2 (&x)[64], bool hb) {
+    if constexpr (K < 64) {
+        const float2 mine = hb ? w256<2 * K, false>(x[K]) : x[K];
+        const float2 oth = swap_pair(mine);
+        x[K] = hb ? csub(oth, mine) : cadd(mine, oth);
+        if constexpr ((K & 15) == 15) sched_fence();
+        combine_fwd<K + 1>(x, hb);
+    }
+}
+
+// inverse split across the pair: A: E'[k] = Z[k] + Z[k+64], B: O'[k] = (Z[k] - Z[k+64]) W128^-k
+template <int K>
+__device__ __forceinline__ void split_inv(float2 (&x)[64], bool hb) {
+    if constexpr (K < 64) {
+        const float2 mine = x[K];
+        const float2 oth = swap_pair(mine);
+        x[K] = hb ? w256<2 * K, true>(csub(oth, mine)) : cadd(mine, oth);
+        if constexpr ((K & 15) == 15) sched_fence();
+        split_inv<K + 1>(x, hb);
+    }
+}
+
+// X[k] = E + W256^k O with E = (Z[k] + conj Z[128-k])/2, O = (Z[k] - conj Z[128-k])/(2i);
+// k = m (A) or 64 + m (B): W256^(64+m) = -i W256^m.  zq = the partner's register 64-m (raw).
+template <int M>
+__device__ __forceinline__ float2 post_fwd(float2 zk, float2 zq, bool hb) {
+    const float2 zm = cconj(zq);
+    const float2 e = cscale(cadd(zk, zm), 0.5f);
+    const float2 d = csub(zk, zm);
+    float2 o = w256<M, false>(make_float2(0.5f * d.y, -0.5f * d.x));
+    if (hb) o = rot<false>(o);
+    return cadd(e, o);
+}
+
+// Z[k] = E + i O with E = X[k] + conj X[128-k], O = (X[k] - conj X[128-k]) W256^-k; W256^-(64+m) = i W256^-m
+template <int M>
+__device__ __forceinline__ float2 pre_inv(float2 xk, float2 xq, bool hb) {
+    const float2 xm = cconj(xq);
+    const float2 e = cadd(xk, xm);
+    float2 o = w256<M, true>(csub(xk, xm));
+    if (hb) o = rot<true>(o);
+    return make_float2(e.x - o.y, e.y + o.x);
+}
+
+template <int M>
+__device__ __forceinline__ void post_fwd_pairs(float2 (&x)[64], bool hb) {
+    if constexpr (M < 32) {
+        constexpr int Q = 64 - M;
+        const float2 pq = swap_pair(x[Q]), pm = swap_pair(x[M]);
+        x[M] = post_fwd<M>(x[M], pq, hb);
+        x[Q] = post_fwd<Q>(x[Q], pm, hb);
+        if constexpr ((M & 7) == 7) sched_fence();
+        post_fwd_pairs<M + 1>(x, hb);
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void pre_inv_pairs(float2 (&x)[64], bool hb) {
+    if constexpr (M < 32) {
+        constexpr int Q = 64 - M;
+        const float2 pq = swap_pair(x[Q]), pm = swap_pair(x[M]);
+        x[M] = pre_inv<M>(x[M], pq, hb);
+        x[Q] = pre_inv<Q>(x[Q], pm, hb);
+        if constexpr ((M & 7) == 7) sched_fence();
+        pre_inv_pairs<M + 1>(x, hb);
+    }
+}
+
+// z (spatial) -> packed half spectrum, in place
+__device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
+    fft64_reg<false>(S);
+    combine_fwd<0>(S, hb);
+    sched_fence();
+    // k = 0 (A): packed (X[0], X[128]) = (Re Z0 + Im Z0, Re Z0 - Im Z0); k = 64 (B): X[64] = conj Z[64]
+    const float2 z0 = S[0];
+    S[0] = hb ? cconj(z0) : make_float2(z0.x + z0.y, z0.x - z0.y);
+    const float2 p32 = swap_pair(S[32]);
+    S[32] = post_fwd<32>(S[32], p32, hb);
+    post_fwd_pairs<1>(S, hb);
+}
+
+// packed half spectrum -> z (spatial), in place (unnormalised: 256 x)
+__device__ __forceinline__ void line_inverse_pair(float2 (&S)[64], bool hb) {
+    const float2 x0 = S[0];
+    S[0] = hb ? make_float2(2.f * x0.x, -2.f * x0.y) : make_float2(x0.x + x0.y, x0.x - x0.y);
+    const float2 p32 = swap_pair(S[32]);
+    S[32] = pre_inv<32>(S[32], p32, hb);
+    pre_inv_pairs<1>(S, hb);
+    sched_fence();
+    split_inv<0>(S, hb);
+    sched_fence();
+    fft64_reg<true>(S);
+}
+
+}  // namespace admm

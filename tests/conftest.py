@@ -4,6 +4,7 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(REPO, "admm-deconv_amd")
 for p in (os.path.join(REPO, "admm-deconv_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests"), REPO):
     if p not in sys.path:
         sys.path.insert(0, p)
