@@ -20,6 +20,7 @@
 #include "../../include/admm_deconv.h"
 #include "admm_kernels.hip"
 #include "admm_backward.hip"
+#include "plane_api.hpp"
 
 namespace {
 
@@ -39,8 +40,17 @@ int fail(int code, const char* fmt, ...) {
 bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 struct Layout {
-    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, total;
+    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, total;
 };
+
+// The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox;
+// ADMM_FUSED=0 forces the 2-pass path (tests compare the two).
+bool fused_shape(int M, int N, bool iso) { return M == 256 && N == 256 && !iso; }
+bool fused_enabled() {
+    const char* e = getenv("ADMM_FUSED");
+    return !(e && e[0] == '0');
+}
+size_t fused_tables_bytes() { return admm::plane::tables_bytes(); }
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
@@ -66,6 +76,7 @@ Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.spec1 = take(planes * MN * 4);
     L.fmap = iso ? take(MN * 4) : 0;
     L.part = iso ? take(((planes + kIsoGroup - 1) / kIsoGroup) * MN * 4) : 0;
+    L.F = fused_shape(M, N, iso) ? take(fused_tables_bytes()) : 0;
     L.total = off;
     return L;
 }
@@ -340,6 +351,19 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         return ADMM_OK;
     }
 
+    if (fused_shape(M, N, iso != 0) && !tr.s && !tr.v && fused_enabled()) {
+        // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
+        // spec0, lane-native s in sA
+        namespace pk = admm::plane;
+        void* tables = ws + lay.F;
+        rc = ln.run(ADMM_K_SETUP, [&] { (void)pk::launch_tables(Ct, Gt, tables, s); });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_PLANE, [&] {
+            (void)pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), tau, rho, maxit,
+                                   planes, s);
+        });
+        return rc;
+    }
     const int T = line_T(M, N);
     const int KB = column_KB(M, N);
     const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "line_pair.hpp"
+#include "plane_kernel.hip"
 
 namespace {
 
@@ -36,6 +37,23 @@ __global__ __launch_bounds__(512) void pair_inv_kernel(const float2* __restrict_
 }  // namespace
 
 extern "C" {
+// fused plane kernel (no PSF) with per-phase dumps of plane 0: dbg holds (4K) x 64 x 512 float2.
+// Cf/C0b must be the lane-native tables; hln/sln workspaces as in admm_capi.hip.
+int devtest_plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,
+                        float rho, int K, int planes, float* dbg) {
+    namespace pk = admm::plane;
+    (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pk::kLdsBytes);
+    hipLaunchKernelGGL((pk::plane256_kernel<false, true>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
+                       nullptr, nullptr, reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
+                       reinterpret_cast<float2*>(dbg));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+int devtest_plane_tables(const float* Ct, float* Cf, float* C0b) {
+    namespace pk = admm::plane;
+    hipLaunchKernelGGL(pk::tables_kernel, dim3(pk::kTab / 256), dim3(256), 0, 0, Ct, nullptr, Cf, C0b, nullptr, nullptr);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
 // rows must be a multiple of 256; device pointers; synchronous
 int devtest_pair_forward(const float* x, float* spec, int rows) {
     pair_fwd_kernel<<<rows / 256, 512>>>(x, reinterpret_cast<float2*>(spec));

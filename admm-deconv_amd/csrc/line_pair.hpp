@@ -43,48 +43,66 @@ __device__ __forceinline__ float2 w256(float2 v) {
     }
 }
 
-// exchange with the partner lane (lane ^ 1) -- DPP quad_perm [1,0,3,2]
+// exchange with the partner lane (lane ^ 1) -- DPP quad_perm [1,0,3,2].
+// The empty volatile asm pins the swap's input at its place in the source order: without it
+// instruction selection hoists all DPP moves of a transform to its start (~100 extra live VGPRs ->
+// scratch spills), ignoring the sched_barrier fences that only bind the machine scheduler.
+#ifdef ADMM_SWAP_BPERMUTE
+__device__ __forceinline__ float swapf(float v) { return __shfl_xor(v, 1); }
+__device__ __forceinline__ float2 swap_pair(float2 v) { return make_float2(__shfl_xor(v.x, 1), __shfl_xor(v.y, 1)); }
+#else
 __device__ __forceinline__ float swapf(float v) {
+    __asm__ volatile("" : "+v"(v));
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
-__device__ __forceinline__ float2 swap_pair(float2 v) { return make_float2(swapf(v.x), swapf(v.y)); }
+__device__ __forceinline__ float2 swap_pair(float2 v) {
+    __asm__ volatile("" : "+v"(v.x), "+v"(v.y));
+    return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0xB1, 0xF, 0xF, true)),
+                       __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, true)));
+}
+#endif
 
-// ---- in-register 64-point FFT, natural order in and out: 64 = 4 (n1) x 16 (n2) -----------------
-//   X[k1 + 4 k2] = sum_{n2} W16^{n2 k2} W64^{n2 k1} sum_{n1} x[16 n1 + n2] W4^{n1 k1}
-template <bool INV, int N2>
-__device__ __forceinline__ void fft64_tw(float2 (&t)[16][4]) {
-    t[N2][1] = w256<4 * N2 * 1, INV>(t[N2][1]);
-    t[N2][2] = w256<4 * N2 * 2, INV>(t[N2][2]);
-    t[N2][3] = w256<4 * N2 * 3, INV>(t[N2][3]);
-    if constexpr (N2 + 1 < 16) fft64_tw<INV, N2 + 1>(t);
+// ---- in-register N-point FFT (N = 32 or 64), natural order in and out: N = 4 (n1) x N/4 (n2) -----
+//   X[k1 + 4 k2] = sum_{n2} W_{N/4}^{n2 k2} W_N^{n2 k1} sum_{n1} x[(N/4) n1 + n2] W4^{n1 k1}
+template <int N, bool INV, int N2>
+__device__ __forceinline__ void fftN_tw(float2 (&t)[N / 4][4]) {
+    constexpr int S = 256 / N;
+    t[N2][1] = w256<S * N2 * 1, INV>(t[N2][1]);
+    t[N2][2] = w256<S * N2 * 2, INV>(t[N2][2]);
+    t[N2][3] = w256<S * N2 * 3, INV>(t[N2][3]);
+    if constexpr (N2 + 1 < N / 4) fftN_tw<N, INV, N2 + 1>(t);
 }
 
 // The scheduling fences keep the machine scheduler from interleaving the stages: left free it hoists
 // work across them and needs ~260 VGPRs (spilling at 2 waves/SIMD); fenced it needs ~160.
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
-template <bool INV>
-__device__ __forceinline__ void fft64_reg(float2 (&x)[64]) {
-    float2 t[16][4];
+template <int N, bool INV>
+__device__ __forceinline__ void fft_reg(float2 (&x)[N]) {
+    constexpr int Q = N / 4;
+    float2 t[Q][4];
 #pragma unroll
-    for (int n2 = 0; n2 < 16; ++n2) {
-        t[n2][0] = x[n2]; t[n2][1] = x[16 + n2]; t[n2][2] = x[32 + n2]; t[n2][3] = x[48 + n2];
+    for (int n2 = 0; n2 < Q; ++n2) {
+        t[n2][0] = x[n2]; t[n2][1] = x[Q + n2]; t[n2][2] = x[2 * Q + n2]; t[n2][3] = x[3 * Q + n2];
         dft4<INV>(t[n2][0], t[n2][1], t[n2][2], t[n2][3]);
     }
     sched_fence();
-    fft64_tw<INV, 1>(t);
+    fftN_tw<N, INV, 1>(t);
     sched_fence();
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1) {
-        float2 u[16];
+        float2 u[Q];
 #pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) u[n2] = t[n2][k1];
-        dft<16, INV>(u);
+        for (int n2 = 0; n2 < Q; ++n2) u[n2] = t[n2][k1];
+        dft<Q, INV>(u);
 #pragma unroll
-        for (int k2 = 0; k2 < 16; ++k2) x[k1 + 4 * k2] = u[k2];
+        for (int k2 = 0; k2 < Q; ++k2) x[k1 + 4 * k2] = u[k2];
         sched_fence();
     }
 }
+
+template <bool INV>
+__device__ __forceinline__ void fft64_reg(float2 (&x)[64]) { fft_reg<64, INV>(x); }
 
 // forward DIT combine across the pair: A: Z[k] = E[k] + W128^k O[k], B: Z[k+64] = E[k] - W128^k O[k]
 template <int K>

@@ -1,0 +1,30 @@
+// plane_api.hpp -- host interface of the fused per-plane kernel (plane_launch.hip).
+//
+// The fused kernel lives in its own translation unit because it is compiled WITHOUT packed-FP32
+// VALU ops (-Xclang -target-feature -Xclang -packed-fp32-ops): with ROCm 7.2's gfx950 codegen the
+// register-dense code of this kernel produced nondeterministic lane corruption in v_pk_*_f32 results
+// (lanes 10-15 of a 16-lane group, found with a per-phase state dump).  Without
+// packed FP32 the kernel is bitwise deterministic.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+namespace admm {
+namespace plane {
+
+constexpr int kPlaneM = 256, kPlaneN = 256;
+constexpr int kTabEntries = 2 * 32 * 512;   // lane-native spectral table entries (= 256 x 128)
+
+// bytes of the lane-native tables (Cf, C0b, Gf, G0b) carved from the workspace
+inline size_t tables_bytes() { return (size_t)kTabEntries * 12 + 256 * 12 + 256; }
+
+// Cf/C0b/Gf/G0b from the 2-pass tables Ct/Gt (Gt may be NULL: no PSF)
+hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStream_t s);
+
+// all K >= 1 iterations for `planes` planes of 256 x 256; hln: planes x 256 KiB, sln: planes x 512 KiB
+hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
+                        float tau, float rho, int K, size_t planes, hipStream_t s);
+
+}  // namespace plane
+}  // namespace admm

@@ -1,0 +1,374 @@
+// plane_kernel.hip -- the whole K-iteration anisotropic ADMM solve of one 256 x 256 plane in ONE
+// workgroup (reference: tvd_fft_cpu/tvd_fft_gpu, /root/reference/src/ops/ops.jl:46-93 / :132-176).
+//
+// Why: the 2-pass path (column kernel + line kernel per iteration, admm_kernels.hip) moves the line
+// spectrum through HBM twice per iteration (36 B/px/iter).  Here the spectrum never leaves the CU:
+// 512 threads = 256 lines x a lane pair (line_pair.hpp) hold it in registers; the dim-2 transforms go
+// through a 132 KiB LDS column buffer in two halves of 64 spectral columns.  The only HBM traffic per
+// iteration is the ADMM state s = Dx + u (read + write, 8 B/px each) and H^T y (4 B/px): 20 B/px/iter.
+// Both are kept in a LANE-NATIVE layout -- element (register n, thread t) at [n][t] -- so every wave
+// load/store is one contiguous 1 KiB (s: float4 = (s1, s1', s2, s2') of the lane's 2 pixels).
+//
+// Per iteration (state: S = line spectra of v = H^T y + rho D^T w):
+//   column phase  (x2 halves) rows -> LDS; per column 8 threads: 32-pt FFT in registers, twiddle,
+//                 wave-local LDS exchange, radix-8; x C/(MN) (x-update, ops.jl:86); inverse the same
+//                 way; LDS -> rows.  Column k = 0 holds the packed real pair (X[0], X[M/2]) and is
+//                 separated with its mirror bin (as column_kernel does).
+//   line inverse  -> x (registers, lane A pixels 4n,4n+1 / lane B 4n+2,4n+3)
+//   row update    s = Dx + clip(s_old) (ops.jl:87-92 with u = clip(s)), w = z - u = phi(s),
+//                 v = H^T y + rho D^T w.  Neighbours along dim 1 come from the partner lane (DPP),
+//                 along dim 2 from lanes +-2 (ds_bpermute) and, across waves, from two LDS boundary
+//                 buffers (x of each wave's last line, w1 of each wave's first line).
+//   line forward  -> S
+// With a PSF the block first forms H^T y = F^-1 conj(Sigma_c) F y (ops.jl:71-81) the same way.
+#include "line_pair.hpp"
+
+namespace admm {
+namespace plane {
+
+constexpr int kPT = 512;                 // threads per block
+constexpr int kCS = 264;                 // column stride (float2) in the column buffer; 264 = 8 mod 32
+constexpr int kTQ = 33;                  // twiddle-table / exchange row stride (float2)
+constexpr int kColF2 = 64 * kCS;         // 64 columns (one half) x 256 bins
+constexpr int kTwF2 = 8 * kTQ;
+constexpr int kMirF2 = 256;
+constexpr int kBndF2 = 8 * 2 * 64;       // 8 waves x 2 lanes x 64 registers
+constexpr int kDumF2 = 8 * 128;          // per-wave sink for the branch-free boundary stores
+// mir (column phase, half 0) and the sink (row phase) never live at the same time: aliased.
+constexpr size_t kLdsBytes = (size_t)(kColF2 + kTwF2 + 2 * kBndF2 + kDumF2) * 8;
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+static_assert(kMirF2 <= kDumF2, "mirror buffer aliases the sink");
+constexpr int kTab = 2 * 32 * kPT;       // lane-native spectral table entries (= 256 x 128)
+
+// Buffer access with the per-register offset in an SGPR (soffset): element (n, t) of a lane-native
+// array is voffset = t * size + soffset = n * 512 * size.  With plain global addressing every n needs
+// its own 64-bit VGPR address (the offsets exceed the 13-bit immediate), which costs ~128 VGPRs.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bld4(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+__device__ __forceinline__ float2 bld2(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+__device__ __forceinline__ float bld1(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bst4(rsrc_t r, unsigned vo, unsigned so, float4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
+}
+__device__ __forceinline__ void bst2(rsrc_t r, unsigned vo, unsigned so, float2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
+}
+
+// LDS exchange between lanes of one wave: LDS executes a wave's instructions in order, the wait
+// makes the dependency explicit and the clobber keeps the compiler from reordering around it.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float clip_tau(float v, float tau) { return fminf(fmaxf(v, -tau), tau); }
+// w = z - u with z = ST(s, tau) and u = s - z  (|s| > tau: s - 2 tau sign s, else -s)
+__device__ __forceinline__ float phi_tau(float s, float tau) {
+    return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s;
+}
+
+// Lane-native spectral tables, built once per call from the 2-pass tables Ct/Gt (bin (kj, k) at
+// kj*(M/2+1) + k).  Entry ((half*4 + i)*8 + q2)*512 + t is the multiplier thread t applies to bin
+// kj = q + 8 i + 32 q2 (q = t & 7) of spectral column k = 32 half + (c >> 1) + 64 (c & 1), c = t >> 3.
+// Column 0 (packed X[0] / X[M/2] pair): Cf = (c0 + cL)/2 and C0b[kj] = (c0 - cL)/2 (same for G).
+__global__ __launch_bounds__(256) void tables_kernel(const float* __restrict__ Ct, const float2* __restrict__ Gt,
+                                                     float* __restrict__ Cf, float* __restrict__ C0b,
+                                                     float2* __restrict__ Gf, float2* __restrict__ G0b) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= kTab) return;
+    const int t = idx & 511, q2 = (idx >> 9) & 7, i = (idx >> 12) & 3, half = idx >> 14;
+    const int q = t & 7, c = t >> 3;
+    const int kj = q + 8 * i + 32 * q2;
+    const int H = 129;
+    if (half == 0 && c == 0) {
+        const float c0 = Ct[kj * H], cL = Ct[kj * H + 128];
+        Cf[idx] = 0.5f * (c0 + cL);
+        C0b[kj] = 0.5f * (c0 - cL);
+        if (Gt) {
+            const float2 g0 = Gt[kj * H], gL = Gt[kj * H + 128];
+            Gf[idx] = cscale(cadd(g0, gL), 0.5f);
+            G0b[kj] = cscale(csub(g0, gL), 0.5f);
+        }
+    } else {
+        const int k = 32 * half + (c >> 1) + 64 * (c & 1);
+        Cf[idx] = Ct[kj * H + k];
+        if (Gt) Gf[idx] = Gt[kj * H + k];
+    }
+}
+
+// One half of the column phase: spectral columns k with register m in [32 HALF, 32 HALF + 32).
+// MODE 0: real multiplier Cf (x-update); MODE 1: complex multiplier Gf (H^T y).
+template <int MODE, int HALF>
+__device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, const float2* tw,
+                                            float2* mir, rsrc_t Cf, const float* __restrict__ C0b,
+                                            rsrc_t Gf, const float2* __restrict__ G0b, int t, bool hb) {
+    const int r = t >> 1;
+    const int q = t & 7, c = t >> 3;
+    // multipliers for this thread's 32 bins (coalesced, L2-resident; issued before the LDS work)
+    float cf[MODE == 0 ? 32 : 1];
+    float2 gf[MODE == 1 ? 32 : 1];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        if constexpr (MODE == 0) cf[j] = bld1(Cf, t * 4, (HALF * 32 + j) * kPT * 4);
+        else gf[j] = bld2(Gf, t * 8, (HALF * 32 + j) * kPT * 8);
+    }
+    // rows -> LDS: column c = 2 m + hb holds register 32 HALF + m of every line
+#pragma unroll
+    for (int m = 0; m < 32; ++m) colbuf[(2 * m + hb) * kCS + r] = S[32 * HALF + m];
+    __syncthreads();
+    float2* col = colbuf + c * kCS;
+    const float2* twq = tw + q * kTQ;
+    float2 v[32];
+    // forward 256 = 32 (in registers, samples j = 8 n + q) x 8 (across the column's 8 lanes)
+#pragma unroll
+    for (int n = 0; n < 32; ++n) v[n] = col[8 * n + q];
+    fft_reg<32, false>(v);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) col[q * kTQ + k] = cmul(v[k], twq[k]);
+    __syncthreads();
+    float2 u[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) u[i][qq] = col[qq * kTQ + q + 8 * i];
+        dft<8, false>(u[i]);
+    }
+    // u[i][q2] = bin kj = q + 8 i + 32 q2 of this column
+    if (HALF == 0 && c == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) mir[q + 8 * i + 32 * q2] = u[i][q2];
+    }
+    if (HALF == 0) __syncthreads();   // DEBUG: block barrier instead of wave-local ordering
+    if (HALF == 0 && c == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) {
+                const int kj = q + 8 * i + 32 * q2;
+                const float2 zm = cconj(mir[(256 - kj) & 255]);
+                if constexpr (MODE == 0) {
+                    u[i][q2] = cadd(cscale(u[i][q2], cf[i * 8 + q2]), cscale(zm, C0b[kj]));
+                } else {
+                    u[i][q2] = cadd(cmul(u[i][q2], gf[i * 8 + q2]), cmul(zm, G0b[kj]));
+                }
+            }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) {
+                if constexpr (MODE == 0) u[i][q2] = cscale(u[i][q2], cf[i * 8 + q2]);
+                else u[i][q2] = cmul(u[i][q2], gf[i * 8 + q2]);
+            }
+    }
+    // inverse: radix-8 across lanes, exchange, twiddle, 32-pt IFFT
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        dft<8, true>(u[i]);
+#pragma unroll
+        for (int qq = 0; qq < 8; ++qq) col[qq * kTQ + q + 8 * i] = u[i][qq];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = cmul(col[q * kTQ + k], cconj(twq[k]));
+    fft_reg<32, true>(v);
+#pragma unroll
+    for (int n = 0; n < 32; ++n) col[8 * n + q] = v[n];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 32; ++m) S[32 * HALF + m] = colbuf[(2 * m + hb) * kCS + r];
+    __syncthreads();
+}
+
+// v(register n) = H^T y + rho D^T w, with w of registers n and n+1 (the partner lane's pixel after this
+// lane's last pixel lives one register later on lane A).
+__device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, bool hb, bool bot, float rho) {
+    const float recv = swapf(hb ? wn.z : wnext.z);     // w2 at the pixel after this lane's 2nd pixel
+    float w1x = __shfl_down(wn.x, 2), w1y = __shfl_down(wn.y, 2);   // w1 of line r+1
+    if (bot) w1x = w1y = 0.0f;                         // next wave's first line: fixed up after the barrier
+    const float q0 = wn.x - w1x + wn.z - wn.w;
+    const float q1 = wn.y - w1y + wn.w - recv;
+    return make_float2(fmaf(rho, q0, hy.x), fmaf(rho, q1, hy.y));
+}
+
+// x (spatial, registers) -> s_k = Dx + clip(s_{k-1}) stored, S <- v = H^T y + rho D^T phi(s_k).
+// Branch-free inside: the boundary-line LDS traffic is done by every lane (reads broadcast from two
+// addresses, writes of non-boundary lanes go to a per-thread sink) so the chunk loop stays one block.
+template <bool FIRST>
+__device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp, float2* xb,
+                                           float2* wb, float2* sink, int t, bool hb,
+                                           float tau, float rho) {
+    constexpr bool first = FIRST;
+    constexpr int CH = 4;
+    const int lane = t & 63, w = t >> 6;
+    const bool top = lane < 2, bot = lane >= 62;
+    float4 so[CH];
+    float2 hy[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        so[j] = first ? make_float4(0.f, 0.f, 0.f, 0.f) : bld4(sp, t * 16, j * kPT * 16);
+        hy[j] = bld2(hp, t * 8, j * kPT * 8);
+    }
+    if (bot) {
+#pragma unroll
+        for (int n = 0; n < 64; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
+    }
+    __syncthreads();
+    const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
+    // this wave's first line (w1); the other lanes write garbage to sink[w][lane + n] (distinct
+    // addresses per instruction, same immediate offsets as the real stores)
+    float2* wbm = top ? wb + (w * 2 + hb) * 64 : sink + w * 128 + lane;
+    float4 wc[CH + 1];
+    float2 hc[CH + 1];
+    float w2x0 = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 64 / CH; ++g) {
+        const int n0 = g * CH;
+        float4 son[CH];
+        float2 hyn[CH];
+        if (g + 1 < 64 / CH) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                son[j] = first ? make_float4(0.f, 0.f, 0.f, 0.f) : bld4(sp, t * 16, (n0 + CH + j) * kPT * 16);
+                hyn[j] = bld2(hp, t * 8, (n0 + CH + j) * kPT * 8);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int n = n0 + j;
+            const float2 x = S[n];
+            const float xl = swapf(hb ? S[(n + 63) & 63].y : x.y);    // pixel before this lane's first
+            const float2 xub = xbp[n];
+            float2 xu = make_float2(__shfl_up(x.x, 2), __shfl_up(x.y, 2));   // line r-1
+            xu.x = top ? xub.x : xu.x;
+            xu.y = top ? xub.y : xu.y;
+            const float4 uo = make_float4(clip_tau(so[j].x, tau), clip_tau(so[j].y, tau), clip_tau(so[j].z, tau),
+                                          clip_tau(so[j].w, tau));
+            const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
+            bst4(sp, t * 16, n * kPT * 16, s);
+            wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
+            hc[j + 1] = hy[j];
+            wbm[n] = make_float2(wc[j + 1].x, wc[j + 1].y);
+            sched_fence();
+        }
+        if (g == 0) w2x0 = wc[1].z;
+#pragma unroll
+        for (int j = (g == 0 ? 1 : 0); j < CH; ++j) {
+            S[n0 - 1 + j] = finalize(wc[j], wc[j + 1], hc[j], hb, bot, rho);
+            sched_fence();
+        }
+        wc[0] = wc[CH];
+        hc[0] = hc[CH];
+        if (g + 1 < 64 / CH) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) { so[j] = son[j]; hy[j] = hyn[j]; }
+        }
+        sched_fence();
+    }
+    S[63] = finalize(wc[0], make_float4(0.f, 0.f, w2x0, 0.f), hc[0], hb, bot, rho);
+    __syncthreads();
+    if (bot) {
+        const float2* wbn = wb + (((w + 1) & 7) * 2 + hb) * 64;   // next wave's first line
+#pragma unroll
+        for (int n = 0; n < 64; ++n) {
+            const float2 a = wbn[n];
+            S[n].x = fmaf(-rho, a.x, S[n].x);
+            S[n].y = fmaf(-rho, a.y, S[n].y);
+        }
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void column_phase(float2 (&S)[64], float2* colbuf, const float2* tw, float2* mir,
+                                             rsrc_t Cf, const float* C0b, rsrc_t Gf, const float2* G0b,
+                                             int t, bool hb) {
+    column_half<MODE, 0>(S, colbuf, tw, mir, Cf, C0b, Gf, G0b, t, hb);
+    column_half<MODE, 1>(S, colbuf, tw, mir, Cf, C0b, Gf, G0b, t, hb);
+}
+
+// debug aid (devtest only): dump S after each phase of every iteration, plane 0
+template <bool DBG>
+__device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int slot, int t) {
+    if constexpr (DBG) {
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int n = 0; n < 64; ++n) dbg[((size_t)slot * 64 + n) * kPT + t] = S[n];
+        }
+    }
+}
+
+// grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
+template <bool PSF, bool DBG = false>
+__global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__ y, float* __restrict__ x_out,
+                                                       const float* __restrict__ Cf, const float* __restrict__ C0b,
+                                                       const float2* __restrict__ Gf, const float2* __restrict__ G0b,
+                                                       float2* __restrict__ hln, float4* __restrict__ sln, float tau,
+                                                       float rho, int K, float2* dbg = nullptr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* colbuf = reinterpret_cast<float2*>(smem_raw);
+    float2* tw = colbuf + kColF2;
+    float2* xb = tw + kTwF2;
+    float2* wb = xb + kBndF2;
+    float2* sink = wb + kBndF2;
+    float2* mir = sink;
+    const int t = threadIdx.x;
+    const bool hb = t & 1;
+    const int r = t >> 1;
+    const size_t plane = blockIdx.x;
+    if (t < 256) {   // W256^(q k), q = 0..7, k = 0..31 (visible after the first barrier)
+        const int q = t >> 5, k = t & 31;
+        double sn, cs;
+        sincospi((double)(q * k) / 128.0, &sn, &cs);
+        tw[q * kTQ + k] = make_float2((float)cs, (float)-sn);
+    }
+    const float2* yrow = reinterpret_cast<const float2*>(y + plane * 65536 + (size_t)r * 256);
+    float2 S[64];
+#pragma unroll
+    for (int n = 0; n < 64; ++n) S[n] = yrow[2 * n + hb];
+    const rsrc_t hp = make_rsrc(hln + plane * 64 * kPT, 64 * kPT * 8);
+    const rsrc_t sp = make_rsrc(sln + plane * 64 * kPT, 64 * kPT * 16);
+    const rsrc_t cfr = make_rsrc(Cf, kTab * 4);
+    const rsrc_t gfr = make_rsrc(Gf, PSF ? kTab * 8 : 0);
+    if constexpr (PSF) {
+        line_forward_pair(S, hb);
+        column_phase<1>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
+        line_inverse_pair(S, hb);   // = H^T y (the 1/(MN) is in Gf)
+    }
+#pragma unroll
+    for (int n = 0; n < 64; ++n) bst2(hp, t * 8, n * kPT * 8, S[n]);
+    line_forward_pair(S, hb);
+    dbg_dump<DBG>(dbg, S, 0, t);
+    for (int k = 1;; ++k) {
+        column_phase<0>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
+        dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
+        line_inverse_pair(S, hb);
+        dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
+        if (k == K) break;
+        if (k == 1) row_update<true>(S, sp, hp, xb, wb, sink, t, hb, tau, rho);
+        else row_update<false>(S, sp, hp, xb, wb, sink, t, hb, tau, rho);
+        dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
+        line_forward_pair(S, hb);
+        dbg_dump<DBG>(dbg, S, 4 * k, t);
+    }
+    float2* xrow = reinterpret_cast<float2*>(x_out + plane * 65536 + (size_t)r * 256);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) xrow[2 * n + hb] = S[n];
+}
+
+}  // namespace plane
+}  // namespace admm

@@ -1,0 +1,51 @@
+// plane_launch.hip -- translation unit of the fused per-plane kernel (built without packed FP32,
+// see plane_api.hpp) and its host launchers.
+#include "plane_api.hpp"
+#include "plane_kernel.hip"
+
+namespace admm {
+namespace plane {
+
+static_assert(kTab == kTabEntries, "table size");
+
+namespace {
+struct Tables {
+    float* Cf;
+    float* C0b;
+    float2* Gf;
+    float2* G0b;
+};
+Tables carve(const void* base) {
+    float* Cf = static_cast<float*>(const_cast<void*>(base));
+    float* C0b = Cf + kTab;
+    float2* Gf = reinterpret_cast<float2*>(C0b + 256);
+    float2* G0b = Gf + kTab;
+    return {Cf, C0b, Gf, G0b};
+}
+}  // namespace
+
+hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStream_t s) {
+    const Tables t = carve(tables);
+    hipLaunchKernelGGL(tables_kernel, dim3(kTab / 256), dim3(256), 0, s, Ct, Gt, t.Cf, t.C0b, t.Gf, t.G0b);
+    return hipGetLastError();
+}
+
+hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
+                        float tau, float rho, int K, size_t planes, hipStream_t s) {
+    const Tables t = carve(tables);
+    if (psf) {
+        (void)hipFuncSetAttribute((const void*)plane256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf, t.C0b,
+                           t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr);
+    } else {
+        (void)hipFuncSetAttribute((const void*)plane256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf,
+                           t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace plane
+}  // namespace admm

@@ -51,7 +51,8 @@ enum {
     ADMM_K_LINE = 3,    /* line pass: irFFT dim1 -> D -> prox -> dual -> D^T -> +H^T y -> rFFT   */
     ADMM_K_FINAL = 4,   /* last irFFT along dim1, writes x                                       */
     ADMM_K_NORM = 5,    /* isotropic only: pixelnorm over the batch (ops.jl:6)                   */
-    ADMM_K_COUNT = 6
+    ADMM_K_PLANE = 6,   /* fused per-plane solve, all K iterations (256 x 256, anisotropic)      */
+    ADMM_K_COUNT = 7
 };
 
 /* ABI version of the loaded library (== ADMM_ABI_VERSION it was built with). */
