@@ -36,19 +36,35 @@ __global__ __launch_bounds__(512) void pair_inv_kernel(const float2* __restrict_
 
 }  // namespace
 
+template <int MODE>
+int plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,
+                       float rho, int K, int planes, float* dbg) {
+    namespace pk = admm::plane;
+    (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<false, MODE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pk::kLdsBytes);
+    hipLaunchKernelGGL((pk::plane256_kernel<false, MODE>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
+                       nullptr, nullptr, reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
+                       reinterpret_cast<float2*>(dbg));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+
 extern "C" {
 // fused plane kernel (no PSF) with per-phase dumps of plane 0: dbg holds (4K) x 64 x 512 float2.
 // Cf/C0b must be the lane-native tables; hln/sln workspaces as in admm_capi.hip.
 int devtest_plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,
                         float rho, int K, int planes, float* dbg) {
-    namespace pk = admm::plane;
-    (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<false, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)pk::kLdsBytes);
-    hipLaunchKernelGGL((pk::plane256_kernel<false, true>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
-                       nullptr, nullptr, reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
-                       reinterpret_cast<float2*>(dbg));
-    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+    return plane_debug<1>(y, x, Cf, C0b, hln, sln, tau, rho, K, planes, dbg);
 }
+// timing: dbg = planes x 8 waves x 512 u64 clock stamps (slot 4k-3.. as above, 256+k after column half 0)
+int devtest_plane_timing(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln,
+                         float tau, float rho, int K, int planes, float* dbg) {
+    return plane_debug<2>(y, x, Cf, C0b, hln, sln, tau, rho, K, planes, dbg);
+}
+#ifdef PLANE_TS
+int devtest_plane_ts_set(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(admm::plane::g_plane_ts), &buf, sizeof(buf)) == hipSuccess ? 0 : -4;
+}
+#endif
 int devtest_plane_tables(const float* Ct, float* Cf, float* C0b) {
     namespace pk = admm::plane;
     hipLaunchKernelGGL(pk::tables_kernel, dim3(pk::kTab / 256), dim3(256), 0, 0, Ct, nullptr, Cf, C0b, nullptr, nullptr);

@@ -34,8 +34,9 @@ constexpr int kTwF2 = 8 * kTQ;
 constexpr int kMirF2 = 256;
 constexpr int kBndF2 = 8 * 2 * 64;       // 8 waves x 2 lanes x 64 registers
 constexpr int kDumF2 = 8 * 128;          // per-wave sink for the branch-free boundary stores
+constexpr int kC0F2 = 128;               // (c0 - cL)/2 of the packed column, 256 floats (LDS copy of C0b)
 // mir (column phase, half 0) and the sink (row phase) never live at the same time: aliased.
-constexpr size_t kLdsBytes = (size_t)(kColF2 + kTwF2 + 2 * kBndF2 + kDumF2) * 8;
+constexpr size_t kLdsBytes = (size_t)(kColF2 + kTwF2 + 2 * kBndF2 + kDumF2 + kC0F2) * 8;
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 static_assert(kMirF2 <= kDumF2, "mirror buffer aliases the sink");
 constexpr int kTab = 2 * 32 * kPT;       // lane-native spectral table entries (= 256 x 128)
@@ -65,6 +66,20 @@ __device__ __forceinline__ void bst2(rsrc_t r, unsigned vo, unsigned so, float2 
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
 }
 
+// Fine-grained phase stamps (devtest timing builds only: -DPLANE_TS).
+#ifdef PLANE_TS
+__device__ unsigned long long* g_plane_ts;
+#define PLANE_STAMP(slot)                                                                              \
+    do {                                                                                               \
+        if ((threadIdx.x & 63) == 0)                                                                   \
+            g_plane_ts[((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + (slot)] += __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PLANE_STAMP(slot) \
+    do {                  \
+    } while (0)
+#endif
+
 // LDS exchange between lanes of one wave: LDS executes a wave's instructions in order, the wait
 // makes the dependency explicit and the clobber keeps the compiler from reordering around it.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -72,6 +87,14 @@ __device__ __forceinline__ void wave_lds_sync() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Block barrier for LDS hand-offs only.  __syncthreads() carries a workgroup release fence that
+// waits vmcnt(0), i.e. for every outstanding global store (the s state) to drain before the barrier
+// -- which made the store traffic synchronous.  No data moves between threads through global memory
+// in this kernel (each thread re-reads only its own lane-native s / H^T y), so LDS ordering suffices.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ float clip_tau(float v, float tau) { return fminf(fmaxf(v, -tau), tau); }
@@ -113,22 +136,17 @@ __global__ __launch_bounds__(256) void tables_kernel(const float* __restrict__ C
 // MODE 0: real multiplier Cf (x-update); MODE 1: complex multiplier Gf (H^T y).
 template <int MODE, int HALF>
 __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, const float2* tw,
-                                            float2* mir, rsrc_t Cf, const float* __restrict__ C0b,
+                                            float2* mir, rsrc_t Cf, const float* C0b,
                                             rsrc_t Gf, const float2* __restrict__ G0b, int t, bool hb) {
     const int r = t >> 1;
     const int q = t & 7, c = t >> 3;
-    // multipliers for this thread's 32 bins (coalesced, L2-resident; issued before the LDS work)
-    float cf[MODE == 0 ? 32 : 1];
-    float2 gf[MODE == 1 ? 32 : 1];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        if constexpr (MODE == 0) cf[j] = bld1(Cf, t * 4, (HALF * 32 + j) * kPT * 4);
-        else gf[j] = bld2(Gf, t * 8, (HALF * 32 + j) * kPT * 8);
-    }
+    PLANE_STAMP(HALF * 8 + 0);
     // rows -> LDS: column c = 2 m + hb holds register 32 HALF + m of every line
 #pragma unroll
     for (int m = 0; m < 32; ++m) colbuf[(2 * m + hb) * kCS + r] = S[32 * HALF + m];
-    __syncthreads();
+    PLANE_STAMP(HALF * 8 + 1);
+    lds_barrier();
+    PLANE_STAMP(HALF * 8 + 2);
     float2* col = colbuf + c * kCS;
     const float2* twq = tw + q * kTQ;
     float2 v[32];
@@ -136,9 +154,20 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
 #pragma unroll
     for (int n = 0; n < 32; ++n) v[n] = col[8 * n + q];
     fft_reg<32, false>(v);
+    PLANE_STAMP(HALF * 8 + 3);
 #pragma unroll
     for (int k = 0; k < 32; ++k) col[q * kTQ + k] = cmul(v[k], twq[k]);
-    __syncthreads();
+    // multipliers for this thread's 32 bins (coalesced, L2-resident), issued once v is dead so they do
+    // not add to the register peak of the FFT
+    sched_fence();
+    float cf[MODE == 0 ? 32 : 1];
+    float2 gf[MODE == 1 ? 32 : 1];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        if constexpr (MODE == 0) cf[j] = bld1(Cf, t * 4, (HALF * 32 + j) * kPT * 4);
+        else gf[j] = bld2(Gf, t * 8, (HALF * 32 + j) * kPT * 8);
+    }
+    wave_lds_sync();
     float2 u[4][8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -146,36 +175,51 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
         for (int qq = 0; qq < 8; ++qq) u[i][qq] = col[qq * kTQ + q + 8 * i];
         dft<8, false>(u[i]);
     }
-    // u[i][q2] = bin kj = q + 8 i + 32 q2 of this column
-    if (HALF == 0 && c == 0) {
+    PLANE_STAMP(HALF * 8 + 4);
+    // u[i][q2] = bin kj = q + 8 i + 32 q2 of this column.
+    // Column k = 0 carries the packed real pair (X[0], X[M/2]): x(c0+cL)/2 plus (c0-cL)/2 x conj(Z(-kj))
+    // separates them (column_kernel's mirror form).  The mirror bin lives in another lane of the same
+    // column, so wave 0 (columns 0..7) swaps the raw bins through LDS.  The branches are wave-uniform
+    // and the other lanes' stores go to a dummy region: no lane diverges.
+    // wave-uniform (readfirstlane makes it a scalar branch, not an EXEC mask)
+    const bool wave0 = HALF == 0 && __builtin_amdgcn_readfirstlane(t >> 6) == 0;
+    const bool col0 = c == 0;
+    if (wave0) {
+        // bin kj of column 0 goes to mir[kj]; bin 0 also to mir[256] so that the mirror read below,
+        // mir[256 - kj] = mir[(8 - q) + 8 (3 - i) + 32 (7 - q2)], is a lane base + immediate offsets
+        float2* mw = col0 ? mir + q : mir + 512 + q;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int q2 = 0; q2 < 8; ++q2) mir[q + 8 * i + 32 * q2] = u[i][q2];
+            for (int q2 = 0; q2 < 8; ++q2) mw[8 * i + 32 * q2] = u[i][q2];
+        float2* m256 = (col0 && q == 0) ? mir + 256 : mir + 520 + (t & 63);   // others: dummy slots
+        *m256 = u[0][0];
     }
-    if (HALF == 0) __syncthreads();   // DEBUG: block barrier instead of wave-local ordering
-    if (HALF == 0 && c == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2) {
+            if constexpr (MODE == 0) u[i][q2] = cscale(u[i][q2], cf[i * 8 + q2]);
+            else u[i][q2] = cmul(u[i][q2], gf[i * 8 + q2]);
+        }
+    if (wave0) {
+        wave_lds_sync();
+        const float2* mr = mir + (8 - q);
+        const float* c0q = C0b + q;
+        const float2* g0q = G0b + q;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int q2 = 0; q2 < 8; ++q2) {
-                const int kj = q + 8 * i + 32 * q2;
-                const float2 zm = cconj(mir[(256 - kj) & 255]);
-                if constexpr (MODE == 0) {
-                    u[i][q2] = cadd(cscale(u[i][q2], cf[i * 8 + q2]), cscale(zm, C0b[kj]));
-                } else {
-                    u[i][q2] = cadd(cmul(u[i][q2], gf[i * 8 + q2]), cmul(zm, G0b[kj]));
-                }
-            }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int q2 = 0; q2 < 8; ++q2) {
-                if constexpr (MODE == 0) u[i][q2] = cscale(u[i][q2], cf[i * 8 + q2]);
-                else u[i][q2] = cmul(u[i][q2], gf[i * 8 + q2]);
+                const float2 zm = cconj(mr[8 * (3 - i) + 32 * (7 - q2)]);
+                float2 add;
+                if constexpr (MODE == 0) add = cscale(zm, c0q[8 * i + 32 * q2]);
+                else add = cmul(zm, g0q[8 * i + 32 * q2]);
+                u[i][q2].x += col0 ? add.x : 0.0f;
+                u[i][q2].y += col0 ? add.y : 0.0f;
             }
     }
+    PLANE_STAMP(HALF * 8 + 5);
     // inverse: radix-8 across lanes, exchange, twiddle, 32-pt IFFT
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -183,16 +227,18 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
 #pragma unroll
         for (int qq = 0; qq < 8; ++qq) col[qq * kTQ + q + 8 * i] = u[i][qq];
     }
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (int k = 0; k < 32; ++k) v[k] = cmul(col[q * kTQ + k], cconj(twq[k]));
     fft_reg<32, true>(v);
 #pragma unroll
     for (int n = 0; n < 32; ++n) col[8 * n + q] = v[n];
-    __syncthreads();
+    PLANE_STAMP(HALF * 8 + 6);
+    lds_barrier();
+    PLANE_STAMP(HALF * 8 + 7);
 #pragma unroll
     for (int m = 0; m < 32; ++m) S[32 * HALF + m] = colbuf[(2 * m + hb) * kCS + r];
-    __syncthreads();
+    lds_barrier();
 }
 
 // v(register n) = H^T y + rho D^T w, with w of registers n and n+1 (the partner lane's pixel after this
@@ -209,26 +255,37 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 // x (spatial, registers) -> s_k = Dx + clip(s_{k-1}) stored, S <- v = H^T y + rho D^T phi(s_k).
 // Branch-free inside: the boundary-line LDS traffic is done by every lane (reads broadcast from two
 // addresses, writes of non-boundary lanes go to a per-thread sink) so the chunk loop stays one block.
-template <bool FIRST>
+// first: iteration 1, s_{k-1} = 0 (ops.jl:48-49 zero init) -- applied as a select on the clipped
+// value (the workspace holds garbage then), so one copy of this code serves every iteration.
+//
+// Register budget: S (128 VGPRs) is the bulk.  The column buffer is idle here, so x of registers
+// 32..63 is parked in it (per-lane slots stg[m * 512 + t]) while registers 0..31 are processed; at
+// the half-way point the slots swap x[32+m] back in and v[m] out, and v[0..30] return at the end.
+// The chunk loop thus holds ~66 S registers instead of 128.
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp, float2* xb,
-                                           float2* wb, float2* sink, int t, bool hb,
+                                           float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho) {
-    constexpr bool first = FIRST;
-    constexpr int CH = 4;
+    constexpr int CH = 2;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
     float4 so[CH];
     float2 hy[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-        so[j] = first ? make_float4(0.f, 0.f, 0.f, 0.f) : bld4(sp, t * 16, j * kPT * 16);
+        so[j] = bld4(sp, t * 16, j * kPT * 16);
         hy[j] = bld2(hp, t * 8, j * kPT * 8);
     }
+    PLANE_STAMP(16);
     if (bot) {
 #pragma unroll
         for (int n = 0; n < 64; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
     }
-    __syncthreads();
+    float2* stg = colbuf + t;
+    const float x63y = S[63].y;   // lane A's register 0 needs the pixel before it (B's pixel 255)
+#pragma unroll
+    for (int m = 0; m < 32; ++m) stg[m * kPT] = S[32 + m];
+    lds_barrier();
+    PLANE_STAMP(17);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
     // this wave's first line (w1); the other lanes write garbage to sink[w][lane + n] (distinct
     // addresses per instruction, same immediate offsets as the real stores)
@@ -244,23 +301,41 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
         if (g + 1 < 64 / CH) {
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
-                son[j] = first ? make_float4(0.f, 0.f, 0.f, 0.f) : bld4(sp, t * 16, (n0 + CH + j) * kPT * 16);
+#ifndef PLANE_EXPT_NOLOAD
+                son[j] = bld4(sp, t * 16, (n0 + CH + j) * kPT * 16);
                 hyn[j] = bld2(hp, t * 8, (n0 + CH + j) * kPT * 8);
+#else
+                son[j] = make_float4(tau * j, 0.f, 0.f, 0.f);
+                hyn[j] = make_float2(rho * (n0 + j), 0.f);
+#endif
             }
+        }
+        if (n0 == 32) {   // half-way: x[32..63] in, v[0..30] out (x[31] still pending in S[31])
+#pragma unroll
+            for (int m = 0; m < 31; ++m) {
+                const float2 xv = stg[m * kPT];
+                stg[m * kPT] = S[m];
+                S[32 + m] = xv;
+            }
+            S[63] = stg[31 * kPT];
+            sched_fence();
         }
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int n = n0 + j;
             const float2 x = S[n];
-            const float xl = swapf(hb ? S[(n + 63) & 63].y : x.y);    // pixel before this lane's first
+            const float xl = swapf(hb ? (n == 0 ? x63y : S[(n + 63) & 63].y) : x.y);   // pixel before this lane's first
             const float2 xub = xbp[n];
             float2 xu = make_float2(__shfl_up(x.x, 2), __shfl_up(x.y, 2));   // line r-1
             xu.x = top ? xub.x : xu.x;
             xu.y = top ? xub.y : xu.y;
-            const float4 uo = make_float4(clip_tau(so[j].x, tau), clip_tau(so[j].y, tau), clip_tau(so[j].z, tau),
-                                          clip_tau(so[j].w, tau));
+            float4 uo = make_float4(clip_tau(so[j].x, tau), clip_tau(so[j].y, tau), clip_tau(so[j].z, tau),
+                                    clip_tau(so[j].w, tau));
+            if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
+#ifndef PLANE_EXPT_NOSTORE
             bst4(sp, t * 16, n * kPT * 16, s);
+#endif
             wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
             hc[j + 1] = hy[j];
             wbm[n] = make_float2(wc[j + 1].x, wc[j + 1].y);
@@ -281,7 +356,11 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
         sched_fence();
     }
     S[63] = finalize(wc[0], make_float4(0.f, 0.f, w2x0, 0.f), hc[0], hb, bot, rho);
-    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 31; ++m) S[m] = stg[m * kPT];
+    PLANE_STAMP(18);
+    lds_barrier();
+    PLANE_STAMP(19);
     if (bot) {
         const float2* wbn = wb + (((w + 1) & 7) * 2 + hb) * 64;   // next wave's first line
 #pragma unroll
@@ -301,10 +380,16 @@ __device__ __forceinline__ void column_phase(float2 (&S)[64], float2* colbuf, co
     column_half<MODE, 1>(S, colbuf, tw, mir, Cf, C0b, Gf, G0b, t, hb);
 }
 
-// debug aid (devtest only): dump S after each phase of every iteration, plane 0
-template <bool DBG>
+// debug aid (devtest only): DBG == 1 dumps S after each phase of every iteration (plane 0);
+// DBG == 2 records the shader clock at each phase boundary (lane 0 of every wave, every plane).
+template <int DBG>
 __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int slot, int t) {
-    if constexpr (DBG) {
+    if constexpr (DBG == 2) {
+        if ((t & 63) == 0) {
+            const unsigned long long c = __builtin_amdgcn_s_memtime();
+            reinterpret_cast<unsigned long long*>(dbg)[((size_t)blockIdx.x * 8 + (t >> 6)) * 512 + slot] = c;
+        }
+    } else if constexpr (DBG == 1) {
         if (blockIdx.x == 0) {
 #pragma unroll
             for (int n = 0; n < 64; ++n) dbg[((size_t)slot * 64 + n) * kPT + t] = S[n];
@@ -313,7 +398,7 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
 }
 
 // grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
-template <bool PSF, bool DBG = false>
+template <bool PSF, int DBG = 0>
 __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__ y, float* __restrict__ x_out,
                                                        const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
@@ -327,6 +412,8 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     float2* sink = wb + kBndF2;
     float2* mir = sink;
     const int t = threadIdx.x;
+    float* c0l = reinterpret_cast<float*>(sink + kDumF2);   // C0b, read by wave 0 in every column phase
+    if (t < 256) c0l[t] = C0b[t];                             // visible after the first barrier
     const bool hb = t & 1;
     const int r = t >> 1;
     const size_t plane = blockIdx.x;
@@ -354,13 +441,14 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     line_forward_pair(S, hb);
     dbg_dump<DBG>(dbg, S, 0, t);
     for (int k = 1;; ++k) {
-        column_phase<0>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
+        column_half<0, 0>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
+        if constexpr (DBG == 2) dbg_dump<DBG>(dbg, S, 256 + k, t);
+        column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
         line_inverse_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
         if (k == K) break;
-        if (k == 1) row_update<true>(S, sp, hp, xb, wb, sink, t, hb, tau, rho);
-        else row_update<false>(S, sp, hp, xb, wb, sink, t, hb, tau, rho);
+        row_update(S, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
         line_forward_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k, t);
