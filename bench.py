@@ -39,7 +39,14 @@ def canonical_bytes(M, N, K):
     return K * (32 * (M // 2 + 1) * N + 20 * M * N) + 12 * M * N
 
 
-def kernel_bytes_per_plane(M, N):
+def plane_bytes_per_px(K):
+    """Fused per-plane kernel (plane_kernel.hip), HBM bytes per pixel for one K-iteration solve:
+    y in (4) + H^T y out (4) + (K-1) x [H^T y in (4) + s out (8)] + (K-2) x s in (8) + x out (4).
+    The line spectrum never leaves the CU, so this is the algorithm's minimum."""
+    return 12 + 12 * (K - 1) + 8 * max(K - 2, 0)
+
+
+def kernel_bytes_per_plane(M, N, K):
     """Algorithmic bytes per plane for one launch of each kernel class (SURVEY.md s8d split)."""
     H = M // 2 + 1
     return {
@@ -47,6 +54,7 @@ def kernel_bytes_per_plane(M, N):
         "line": 16 * H * N + 20 * M * N,      # spectrum in/out + s in/out (2 ch) + H^T y
         "prep": 8 * M * N + 8 * H * N,        # y in, H^T y out, spectrum out
         "final": 8 * H * N + 4 * M * N,       # spectrum in, x out
+        "plane": plane_bytes_per_px(K) * M * N,   # whole fused solve
     }
 
 
@@ -227,7 +235,7 @@ def main():
         admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws, stream=stream)
     _lib.profile_enable(False)
     planes = B * P
-    kb = kernel_bytes_per_plane(M, N)
+    kb = kernel_bytes_per_plane(M, N, K)
     kernels = {}
     for cls, name in _lib.KERNEL_CLASSES.items():
         ms, n = _lib.profile_get(cls)
@@ -240,6 +248,7 @@ def main():
             e["achieved_GBps"] = kb[name] * planes / (avg_ms * 1e-3) / 1e9
         kernels[name] = e
     dom = max((k for k in kernels if k in kb), key=lambda k: kernels[k]["total_ms_per_solve"])
+    alg_bytes = kb["plane"] * planes if "plane" in kernels else canonical_bytes(M, N, K) * planes
     traffic = load_traffic(args.config, dom)
     ach = kernels[dom]["achieved_GBps"]
     roofline = {
@@ -248,9 +257,13 @@ def main():
         "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
         "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
         "whole_solve": {
-            "canonical_bytes": canonical_bytes(M, N, K) * planes,
-            "achieved_GBps": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9, 1),
-            "frac": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            # the bytes of the path that ran (fused: plane_bytes_per_px; 2-pass: SURVEY s8d canonical)
+            "algorithmic_bytes": alg_bytes,
+            "achieved_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            "frac": round(alg_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            # SURVEY.md s8d's 2-pass figure (spectrum round-trips through HBM twice per iteration)
+            "canonical_2pass_bytes": canonical_bytes(M, N, K) * planes,
+            "canonical_2pass_GBps": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9, 1),
         },
     }
 
