@@ -36,15 +36,16 @@ __global__ __launch_bounds__(512) void pair_inv_kernel(const float2* __restrict_
 
 }  // namespace
 
-template <int MODE>
+template <int MODE, bool PSF = false>
 int plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,
-                       float rho, int K, int planes, float* dbg) {
+                       float rho, int K, int planes, float* dbg, const float* Gf = nullptr, const float* G0b = nullptr) {
     namespace pk = admm::plane;
-    (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<false, MODE>,
+    (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<PSF, MODE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)pk::kLdsBytes);
-    hipLaunchKernelGGL((pk::plane256_kernel<false, MODE>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
-                       nullptr, nullptr, reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
-                       reinterpret_cast<float2*>(dbg));
+    hipLaunchKernelGGL((pk::plane256_kernel<PSF, MODE>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
+                       reinterpret_cast<const float2*>(Gf), reinterpret_cast<const float2*>(G0b),
+                       reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
+                       reinterpret_cast<float2*>(dbg), 0);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
 }
 
@@ -69,6 +70,18 @@ int devtest_plane_tables(const float* Ct, float* Cf, float* C0b) {
     namespace pk = admm::plane;
     hipLaunchKernelGGL(pk::tables_kernel, dim3(pk::kTab / 256), dim3(256), 0, 0, Ct, nullptr, Cf, C0b, nullptr, nullptr);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+// PSF variant: Gt = conj(Sigma_c)/(MN) as float2[256][129]; Gf = kTab float2, G0b = 256 float2
+int devtest_plane_tables_psf(const float* Ct, const float* Gt, float* Cf, float* C0b, float* Gf, float* G0b) {
+    namespace pk = admm::plane;
+    hipLaunchKernelGGL(pk::tables_kernel, dim3(pk::kTab / 256), dim3(256), 0, 0, Ct, reinterpret_cast<const float2*>(Gt),
+                       Cf, C0b, reinterpret_cast<float2*>(Gf), reinterpret_cast<float2*>(G0b));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+int devtest_plane_debug_psf(const float* y, float* x, const float* Cf, const float* C0b, const float* Gf,
+                            const float* G0b, float* hln, float* sln, float tau, float rho, int K, int planes,
+                            float* dbg) {
+    return plane_debug<1, true>(y, x, Cf, C0b, hln, sln, tau, rho, K, planes, dbg, Gf, G0b);
 }
 // rows must be a multiple of 256; device pointers; synchronous
 int devtest_pair_forward(const float* x, float* spec, int rows) {

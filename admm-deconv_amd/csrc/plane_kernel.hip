@@ -265,16 +265,26 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho) {
-    constexpr int CH = 2;
+    constexpr int CH = 2;            // registers per chunk
+#ifndef PLANE_PD
+#define PLANE_PD 1
+#endif
+    // Prefetch distance (chunks in flight).  PD > 1 measured no faster and, with the PSF variant's
+    // register allocation, reproduced the VMEM-overwrites-DPP-source corruption.
+    constexpr int PD = PLANE_PD;
+    constexpr int NCH = 64 / CH;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
-    float4 so[CH];
-    float2 hy[CH];
+    // ring of PD+1 chunk buffers of s_{k-1} and H^T y (compile-time slots: the chunk loop is unrolled)
+    float4 sor[PD + 1][CH];
+    float2 hyr[PD + 1][CH];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        so[j] = bld4(sp, t * 16, j * kPT * 16);
-        hy[j] = bld2(hp, t * 8, j * kPT * 8);
-    }
+    for (int g = 0; g < PD; ++g)
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            sor[g][j] = bld4(sp, t * 16, (g * CH + j) * kPT * 16);
+            hyr[g][j] = bld2(hp, t * 8, (g * CH + j) * kPT * 8);
+        }
     PLANE_STAMP(16);
     if (bot) {
 #pragma unroll
@@ -294,20 +304,18 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
     float2 hc[CH + 1];
     float w2x0 = 0.0f;
 #pragma unroll
-    for (int g = 0; g < 64 / CH; ++g) {
+    for (int g = 0; g < NCH; ++g) {
         const int n0 = g * CH;
-        float4 son[CH];
-        float2 hyn[CH];
-        if (g + 1 < 64 / CH) {
+        if (g + PD < NCH) {
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
-#ifndef PLANE_EXPT_NOLOAD
-                son[j] = bld4(sp, t * 16, (n0 + CH + j) * kPT * 16);
-                hyn[j] = bld2(hp, t * 8, (n0 + CH + j) * kPT * 8);
-#else
-                son[j] = make_float4(tau * j, 0.f, 0.f, 0.f);
-                hyn[j] = make_float2(rho * (n0 + j), 0.f);
-#endif
+                // keep the slot's old value live up to here, so its registers are not recycled as
+                // temporaries (and read by VALU/DPP) just before this load overwrites them
+                __asm__ volatile("" ::"v"(sor[(g + PD) % (PD + 1)][j].x), "v"(sor[(g + PD) % (PD + 1)][j].y),
+                                 "v"(sor[(g + PD) % (PD + 1)][j].z), "v"(sor[(g + PD) % (PD + 1)][j].w),
+                                 "v"(hyr[(g + PD) % (PD + 1)][j].x), "v"(hyr[(g + PD) % (PD + 1)][j].y));
+                sor[(g + PD) % (PD + 1)][j] = bld4(sp, t * 16, ((g + PD) * CH + j) * kPT * 16);
+                hyr[(g + PD) % (PD + 1)][j] = bld2(hp, t * 8, ((g + PD) * CH + j) * kPT * 8);
             }
         }
         if (n0 == 32) {   // half-way: x[32..63] in, v[0..30] out (x[31] still pending in S[31])
@@ -323,21 +331,21 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int n = n0 + j;
+            const float4 so = sor[g % (PD + 1)][j];
             const float2 x = S[n];
             const float xl = swapf(hb ? (n == 0 ? x63y : S[(n + 63) & 63].y) : x.y);   // pixel before this lane's first
             const float2 xub = xbp[n];
             float2 xu = make_float2(__shfl_up(x.x, 2), __shfl_up(x.y, 2));   // line r-1
             xu.x = top ? xub.x : xu.x;
             xu.y = top ? xub.y : xu.y;
-            float4 uo = make_float4(clip_tau(so[j].x, tau), clip_tau(so[j].y, tau), clip_tau(so[j].z, tau),
-                                    clip_tau(so[j].w, tau));
+            float4 uo = make_float4(clip_tau(so.x, tau), clip_tau(so.y, tau), clip_tau(so.z, tau), clip_tau(so.w, tau));
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
 #ifndef PLANE_EXPT_NOSTORE
             bst4(sp, t * 16, n * kPT * 16, s);
 #endif
             wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
-            hc[j + 1] = hy[j];
+            hc[j + 1] = hyr[g % (PD + 1)][j];
             wbm[n] = make_float2(wc[j + 1].x, wc[j + 1].y);
             sched_fence();
         }
@@ -349,10 +357,6 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
         }
         wc[0] = wc[CH];
         hc[0] = hc[CH];
-        if (g + 1 < 64 / CH) {
-#pragma unroll
-            for (int j = 0; j < CH; ++j) { so[j] = son[j]; hy[j] = hyn[j]; }
-        }
         sched_fence();
     }
     S[63] = finalize(wc[0], make_float4(0.f, 0.f, w2x0, 0.f), hc[0], hb, bot, rho);
@@ -403,7 +407,13 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
                                                        const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
                                                        float2* __restrict__ hln, float4* __restrict__ sln, float tau,
-                                                       float rho, int K, float2* dbg = nullptr) {
+                                                       float rho, int K, float2* dbg = nullptr, int stagger_ticks = 0) {
+    // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
+    // late, so that the memory-heavy row phases of two groups of CUs interleave.
+    if (stagger_ticks > 0 && (blockIdx.x & 1)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger_ticks) __builtin_amdgcn_s_sleep(10);
+    }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* colbuf = reinterpret_cast<float2*>(smem_raw);
     float2* tw = colbuf + kColF2;

@@ -1,5 +1,7 @@
 // plane_launch.hip -- translation unit of the fused per-plane kernel (built without packed FP32,
 // see plane_api.hpp) and its host launchers.
+#include <cstdlib>
+
 #include "plane_api.hpp"
 #include "plane_kernel.hip"
 
@@ -33,16 +35,20 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
                         float tau, float rho, int K, size_t planes, hipStream_t s) {
     const Tables t = carve(tables);
+    static const int stagger = [] {
+        const char* e = getenv("ADMM_PLANE_STAGGER");   // experiment knob: realtime ticks (10 ns)
+        return e ? atoi(e) : 0;
+    }();
     if (psf) {
         (void)hipFuncSetAttribute((const void*)plane256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kLdsBytes);
         hipLaunchKernelGGL(plane256_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf, t.C0b,
-                           t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr);
+                           t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger);
     } else {
         (void)hipFuncSetAttribute((const void*)plane256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)kLdsBytes);
         hipLaunchKernelGGL(plane256_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf,
-                           t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr);
+                           t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger);
     }
     return hipGetLastError();
 }

@@ -67,3 +67,21 @@ def test_plane_deterministic_and_batch_invariant(dev):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert torch.equal(a, part)
+
+
+@pytest.mark.parametrize("psf", [True, False], ids=["psf", "nopsf"])
+def test_plane_census_full_batch(dev, psf):
+    """A whole c2 batch (512 planes) twice: every plane equal to the 2-pass path within the parity
+    tolerance and bitwise equal across runs.  Guards against the lane-corruption hazard class described
+    in DESIGN.md s4 (it showed as a few bad planes per launch, varying run to run)."""
+    h = synth.gaussian_psf(15, 2.5) if psf else None
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    y = torch.from_numpy(synth.make_batch(64, 256, 256, h)).to(dev).repeat(8, 1, 1, 1).contiguous()
+    with fused_off():
+        ref = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 6)
+    a = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 6)
+    b = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 6)
+    torch.cuda.synchronize()
+    rel = ((a - ref).flatten(1).norm(dim=1) / ref.flatten(1).norm(dim=1)).cpu()
+    assert float(rel.max()) <= 1e-5, f"worst plane rel-L2 {float(rel.max()):.3e}, bad planes {int((rel > 1e-5).sum())}"
+    assert torch.equal(a, b)
