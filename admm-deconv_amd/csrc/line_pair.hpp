@@ -174,6 +174,31 @@ __device__ __forceinline__ void pre_inv_pairs(float2 (&x)[64], bool hb) {
     }
 }
 
+// one register of the inverse split (see split_inv)
+template <int K>
+__device__ __forceinline__ void split_one(float2 (&x)[64], bool hb) {
+    const float2 mine = x[K];
+    const float2 oth = swap_pair(mine);
+    x[K] = hb ? w256<2 * K, true>(csub(oth, mine)) : cadd(mine, oth);
+}
+
+// pre-processing of pair (M, 64-M) fused with the split of both registers: each register is final for
+// the 64-point IFFT as soon as its pair is done, which keeps the live set small (pre then split as two
+// sweeps needed ~256 VGPRs and spilled; fused it fits with the FFT's own peak)
+template <int M>
+__device__ __forceinline__ void pre_split_pairs(float2 (&x)[64], bool hb) {
+    if constexpr (M < 32) {
+        constexpr int Q = 64 - M;
+        const float2 pq = swap_pair(x[Q]), pm = swap_pair(x[M]);
+        x[M] = pre_inv<M>(x[M], pq, hb);
+        x[Q] = pre_inv<Q>(x[Q], pm, hb);
+        split_one<M>(x, hb);
+        split_one<Q>(x, hb);
+        if constexpr ((M & 3) == 3) sched_fence();
+        pre_split_pairs<M + 1>(x, hb);
+    }
+}
+
 // z (spatial) -> packed half spectrum, in place
 __device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
     fft64_reg<false>(S);
@@ -191,11 +216,11 @@ __device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
 __device__ __forceinline__ void line_inverse_pair(float2 (&S)[64], bool hb) {
     const float2 x0 = S[0];
     S[0] = hb ? make_float2(2.f * x0.x, -2.f * x0.y) : make_float2(x0.x + x0.y, x0.x - x0.y);
+    split_one<0>(S, hb);
     const float2 p32 = swap_pair(S[32]);
     S[32] = pre_inv<32>(S[32], p32, hb);
-    pre_inv_pairs<1>(S, hb);
-    sched_fence();
-    split_inv<0>(S, hb);
+    split_one<32>(S, hb);
+    pre_split_pairs<1>(S, hb);
     sched_fence();
     fft64_reg<true>(S);
 }

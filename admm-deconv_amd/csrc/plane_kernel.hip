@@ -141,9 +141,14 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     const int r = t >> 1;
     const int q = t & 7, c = t >> 3;
     PLANE_STAMP(HALF * 8 + 0);
-    // rows -> LDS: column c = 2 m + hb holds register 32 HALF + m of every line
+    // rows -> LDS: column c = 2 m + hb holds register 32 HALF + m of every line.  Two bases (m < 16,
+    // m >= 16) keep every access base + 16-bit immediate (m * 4224 B would overflow one base).
+    float2* rlo = colbuf + hb * kCS + r;
+    float2* rhi = rlo + 32 * kCS;
 #pragma unroll
-    for (int m = 0; m < 32; ++m) colbuf[(2 * m + hb) * kCS + r] = S[32 * HALF + m];
+    for (int m = 0; m < 16; ++m) rlo[2 * m * kCS] = S[32 * HALF + m];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) rhi[2 * m * kCS] = S[32 * HALF + 16 + m];
     PLANE_STAMP(HALF * 8 + 1);
     lds_barrier();
     PLANE_STAMP(HALF * 8 + 2);
@@ -237,7 +242,9 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     lds_barrier();
     PLANE_STAMP(HALF * 8 + 7);
 #pragma unroll
-    for (int m = 0; m < 32; ++m) S[32 * HALF + m] = colbuf[(2 * m + hb) * kCS + r];
+    for (int m = 0; m < 16; ++m) S[32 * HALF + m] = rlo[2 * m * kCS];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) S[32 * HALF + 16 + m] = rhi[2 * m * kCS];
     lds_barrier();
 }
 
@@ -290,10 +297,14 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
 #pragma unroll
         for (int n = 0; n < 64; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
     }
+    // staging slots stg[m * 512 + t]: two bases keep the offsets within the 16-bit ds immediate
     float2* stg = colbuf + t;
+    float2* stg2 = stg + 16 * kPT;
     const float x63y = S[63].y;   // lane A's register 0 needs the pixel before it (B's pixel 255)
 #pragma unroll
-    for (int m = 0; m < 32; ++m) stg[m * kPT] = S[32 + m];
+    for (int m = 0; m < 16; ++m) stg[m * kPT] = S[32 + m];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) stg2[m * kPT] = S[48 + m];
     lds_barrier();
     PLANE_STAMP(17);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
@@ -320,12 +331,18 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
         }
         if (n0 == 32) {   // half-way: x[32..63] in, v[0..30] out (x[31] still pending in S[31])
 #pragma unroll
-            for (int m = 0; m < 31; ++m) {
+            for (int m = 0; m < 16; ++m) {
                 const float2 xv = stg[m * kPT];
                 stg[m * kPT] = S[m];
                 S[32 + m] = xv;
             }
-            S[63] = stg[31 * kPT];
+#pragma unroll
+            for (int m = 0; m < 15; ++m) {
+                const float2 xv = stg2[m * kPT];
+                stg2[m * kPT] = S[16 + m];
+                S[48 + m] = xv;
+            }
+            S[63] = stg2[15 * kPT];
             sched_fence();
         }
 #pragma unroll
@@ -361,7 +378,9 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
     }
     S[63] = finalize(wc[0], make_float4(0.f, 0.f, w2x0, 0.f), hc[0], hb, bot, rho);
 #pragma unroll
-    for (int m = 0; m < 31; ++m) S[m] = stg[m * kPT];
+    for (int m = 0; m < 16; ++m) S[m] = stg[m * kPT];
+#pragma unroll
+    for (int m = 0; m < 15; ++m) S[16 + m] = stg2[m * kPT];
     PLANE_STAMP(18);
     lds_barrier();
     PLANE_STAMP(19);
