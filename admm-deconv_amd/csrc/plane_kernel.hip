@@ -285,13 +285,6 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
     // ring of PD+1 chunk buffers of s_{k-1} and H^T y (compile-time slots: the chunk loop is unrolled)
     float4 sor[PD + 1][CH];
     float2 hyr[PD + 1][CH];
-#pragma unroll
-    for (int g = 0; g < PD; ++g)
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            sor[g][j] = bld4(sp, t * 16, (g * CH + j) * kPT * 16);
-            hyr[g][j] = bld2(hp, t * 8, (g * CH + j) * kPT * 8);
-        }
     PLANE_STAMP(16);
     if (bot) {
 #pragma unroll
@@ -306,6 +299,16 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
 #pragma unroll
     for (int m = 0; m < 16; ++m) stg2[m * kPT] = S[48 + m];
     lds_barrier();
+    // prologue loads after the staging: issued earlier they made every spill reload around the line
+    // inverse wait for them (one in-order vmcnt)
+    sched_fence();
+#pragma unroll
+    for (int g = 0; g < PD; ++g)
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            sor[g][j] = bld4(sp, t * 16, (g * CH + j) * kPT * 16);
+            hyr[g][j] = bld2(hp, t * 8, (g * CH + j) * kPT * 8);
+        }
     PLANE_STAMP(17);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
     // this wave's first line (w1); the other lanes write garbage to sink[w][lane + n] (distinct
@@ -318,6 +321,11 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
     for (int g = 0; g < NCH; ++g) {
         const int n0 = g * CH;
         if (g + PD < NCH) {
+#ifdef PLANE_VMEM_NOPS
+            // wait states between the last VALU/DPP reads and the loads that overwrite the slot
+            sched_fence();
+            __asm__ volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 // keep the slot's old value live up to here, so its registers are not recycled as

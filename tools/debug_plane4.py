@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(REPO, "admm-deconv_amd"))
 from admm_deconv import synth  # noqa: E402
 
 dev = torch.device("cuda:0")
-lib = ctypes.CDLL(os.path.join(REPO, "admm-deconv_amd", "libadmm_devtest.so"))
+lib = ctypes.CDLL(os.path.join(REPO, "admm-deconv_amd", sys.argv[2] if len(sys.argv) > 2 else "libadmm_devtest.so"))
 P = ctypes.c_void_p
 lib.devtest_plane_debug.argtypes = [P, P, P, P, P, P, ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int, P]
 lib.devtest_plane_tables.argtypes = [P, P, P]
