@@ -179,7 +179,7 @@ def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, wo
     y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: scalars or
     1-element tensors; h: PSF (kw,kh) (= Julia (kh,kw)) or None/empty.  Returns a new tensor.
     Differentiable (y, lam, rho, h) when autograd is recording and any of them requires grad
-    (anisotropic prox); the gradient is the exact adjoint of the K unrolled iterations."""
+    (either prox); the gradient is the exact adjoint of the K unrolled iterations."""
     tensors = [t for t in (y, lam, rho, h) if isinstance(t, torch.Tensor)]
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
         dev = y.device

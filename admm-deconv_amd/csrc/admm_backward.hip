@@ -338,4 +338,273 @@ __global__ void grads_final_kernel(const double* __restrict__ rt, const double* 
     if (h_bar && t < ntaps) h_bar[t] = (float)(hb_corr[t] + (hb_A ? hb_A[t] : 0.0));
 }
 
+
+// ==============================================================================================
+// Isotropic (BT) adjoint (tests/kernel_model.py tvd_model_grads(iso=True) is the restatement).
+// With f = max(1 - tau/Nrm, 0), Nrm(pixel) = sqrt(sum over ALL planes and both channels of s^2):
+// w = (2f - 1) s, u = (1 - f) s, and one reverse step needs the batch reduction
+//   R(pixel) = sum_{planes, channels} s_{k-1} (2 wbar - sbar_k),   wbar = rho D vbar_k
+//   sbar_{k-1} = (2f - 1) wbar + (1 - f) sbar_k + [Nrm > tau] (tau / Nrm^3) R s_{k-1}
+//   tau_bar  += sum_pixels [Nrm > tau] (-R / Nrm)
+// so the step runs as ISO_ADJ_A (per plane group: vbar, D vbar, rho_bar, Vsum, wbar, partial R) ->
+// ISO_ADJ_R (R map, tau_bar) -> ISO_ADJ_B (per plane: sbar_{k-1}, D^T, rFFT) -- the forward's
+// iso_a -> iso_r -> iso_b shape.  nrm1 is the saved Nrm of iteration k-1.
+// ==============================================================================================
+__device__ __forceinline__ float bt_factor(float nrm, float tau) { return max0_nan(1.0f - tau / nrm); }
+
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __restrict__ spec1,
+                                                             const float* __restrict__ sk1, const float* __restrict__ sk,
+                                                             const float* __restrict__ xK,
+                                                             const float* __restrict__ nrm1, const float* __restrict__ nrm0,
+                                                             const float* __restrict__ sb_in, float* __restrict__ wbar,
+                                                             float* __restrict__ vsum, float* __restrict__ rpartial,
+                                                             double* __restrict__ part, const float2* __restrict__ twM,
+                                                             int N, int planes, int G, float tau, float rho,
+                                                             int first_k, int last_k) {
+    // nrm1 = Nrm_{k-1} (k >= 2), nrm0 = Nrm_{k-2} (k >= 3; for D x_k = s_k - psi(s_{k-1}) we need f_{k-1}
+    // only: nrm0 is unused but kept for symmetry of the call -- psi(s_{k-1}) uses nrm1)
+    (void)nrm0;
+    constexpr int M = 2 * L;
+    constexpr int M4 = M / 4;
+    constexpr int TH = T + 1;
+    constexpr int NE = T * M4;
+    constexpr int NIT = (NE + kThreads - 1) / kThreads;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float2* X = tw + M;
+    float2* Bf = X + TH * L;
+    float2* Cf = Bf + TH * L;
+    double* red = reinterpret_cast<double*>(Cf + TH * L);
+    const int j0 = blockIdx.x * T;
+    const int grp = blockIdx.y;
+    const size_t MN = (size_t)M * N;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    float4 racc[NIT], fo[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        racc[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        fo[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int idx = tid + it * kThreads;
+        if (!first_k && idx < NE) {
+            const int t = idx / M4, i = (idx - t * M4) * 4;
+            const float4 nn = *reinterpret_cast<const float4*>(nrm1 + (size_t)(j0 + t) * M + i);
+            fo[it] = make_float4(bt_factor(nn.x, tau), bt_factor(nn.y, tau), bt_factor(nn.z, tau), bt_factor(nn.w, tau));
+        }
+    }
+    float rho_acc = 0.0f;
+    const int p_end = min(planes, (grp + 1) * G);
+    for (int plane = grp * G; plane < p_end; ++plane) {
+        __syncthreads();
+        load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
+        __syncthreads();
+        auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
+        float2* Xr;
+        if constexpr (Plan<L>::P == 1) {
+            Xr = Bf;
+            fpass<L, L, 0, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+        } else if constexpr (Plan<L>::P == 2) {
+            Xr = X;
+            fft_plan<L, false, true, 2>(TH, tw, Bf, Cf, L, uload, LdsIO{X, L});
+        } else {
+            Xr = Bf;
+            plan_pass<L, 0, false, true, 2>(TH, tw, uload, LdsIO{Bf, L});
+            __syncthreads();
+            plan_pass<L, 1, false, true, 2>(TH, tw, LdsIO{Bf, L}, LdsIO{Cf, L});
+            __syncthreads();
+            plan_pass<L, 2, false, true, 2>(TH, tw, LdsIO{Cf, L}, LdsIO{Bf, L});
+        }
+        __syncthreads();
+        const float* vb = reinterpret_cast<const float*>(Xr);   // lines j0-1 .. j0+T-1
+        const size_t poff = (size_t)plane * 2 * MN;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int idx = tid + it * kThreads;
+            if (idx >= NE) continue;
+            const int t = idx / M4, i = (idx - t * M4) * 4;
+            const size_t off = (size_t)(j0 + t) * M + i;
+            const float4 vc = *reinterpret_cast<const float4*>(vb + (t + 1) * M + i);
+            const float4 vp = *reinterpret_cast<const float4*>(vb + t * M + i);
+            const float vl = vb[(t + 1) * M + ((i - 1) & (M - 1))];
+            const float dv0[4] = {vc.x - vp.x, vc.y - vp.y, vc.z - vp.z, vc.w - vp.w};
+            const float dv1[4] = {vc.x - vl, vc.y - vc.x, vc.z - vc.y, vc.w - vc.z};
+            const float f4[4] = {fo[it].x, fo[it].y, fo[it].z, fo[it].w};
+            float a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};   // s_{k-1}
+            if (!first_k) {
+                const float4 a = *reinterpret_cast<const float4*>(sk1 + poff + off);
+                const float4 b = *reinterpret_cast<const float4*>(sk1 + poff + MN + off);
+                a0[0] = a.x; a0[1] = a.y; a0[2] = a.z; a0[3] = a.w;
+                a1[0] = b.x; a1[1] = b.y; a1[2] = b.z; a1[3] = b.w;
+            }
+            // ---- rho_bar: -<D vbar, D x_k> ----
+            float dx0[4], dx1[4];
+            if (last_k) {
+                const float* xp = xK + (size_t)plane * MN;
+                const float4 xc = *reinterpret_cast<const float4*>(xp + off);
+                const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
+                const float xl = xp[(size_t)(j0 + t) * M + ((i - 1) & (M - 1))];
+                dx0[0] = xc.x - xq.x; dx0[1] = xc.y - xq.y; dx0[2] = xc.z - xq.z; dx0[3] = xc.w - xq.w;
+                dx1[0] = xc.x - xl; dx1[1] = xc.y - xc.x; dx1[2] = xc.z - xc.y; dx1[3] = xc.w - xc.z;
+            } else {
+                const float4 a = *reinterpret_cast<const float4*>(sk + poff + off);
+                const float4 b = *reinterpret_cast<const float4*>(sk + poff + MN + off);
+                const float c0[4] = {a.x, a.y, a.z, a.w}, c1[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {   // D x_k = s_k - psi(s_{k-1}) = s_k - (1 - f_{k-1}) s_{k-1}
+                    dx0[q] = c0[q] - (1.0f - f4[q]) * a0[q];
+                    dx1[q] = c1[q] - (1.0f - f4[q]) * a1[q];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rho_acc -= dv0[q] * dx0[q] + dv1[q] * dx1[q];
+            float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
+            float4 acc = *vs;
+            acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
+            *vs = acc;
+            if (!first_k) {
+                float b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};   // sbar_k
+                if (sb_in) {
+                    const float4 a = *reinterpret_cast<const float4*>(sb_in + poff + off);
+                    const float4 b = *reinterpret_cast<const float4*>(sb_in + poff + MN + off);
+                    b0[0] = a.x; b0[1] = a.y; b0[2] = a.z; b0[3] = a.w;
+                    b1[0] = b.x; b1[1] = b.y; b1[2] = b.z; b1[3] = b.w;
+                }
+                float w0[4], w1[4], rr[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    w0[q] = rho * dv0[q];
+                    w1[q] = rho * dv1[q];
+                    const float ph = 2.0f * f4[q] - 1.0f;   // phi(s) = (2f - 1) s
+                    rho_acc += ph * (a0[q] * dv0[q] + a1[q] * dv1[q]);
+                    rr[q] = a0[q] * (2.0f * w0[q] - b0[q]) + a1[q] * (2.0f * w1[q] - b1[q]);
+                }
+                *reinterpret_cast<float4*>(wbar + poff + off) = make_float4(w0[0], w0[1], w0[2], w0[3]);
+                *reinterpret_cast<float4*>(wbar + poff + MN + off) = make_float4(w1[0], w1[1], w1[2], w1[3]);
+                racc[it].x += rr[0]; racc[it].y += rr[1]; racc[it].z += rr[2]; racc[it].w += rr[3];
+            }
+        }
+    }
+    if (!first_k) {
+        float* pp = rpartial + (size_t)grp * MN;
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int idx = tid + it * kThreads;
+            if (idx < NE) {
+                const int t = idx / M4, i = (idx - t * M4) * 4;
+                *reinterpret_cast<float4*>(pp + (size_t)(j0 + t) * M + i) = racc[it];
+            }
+        }
+    }
+    __syncthreads();
+    block_sum2(rho_acc, 0.0f, part + 2 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x), red);
+}
+
+// R map = sum over plane groups of the partial sums; tau_bar partials (block-reduced, one pair per block)
+__global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __restrict__ rpartial, float* __restrict__ Rmap,
+                                                             const float* __restrict__ nrm1, int ngroups, size_t MN,
+                                                             float tau, double* __restrict__ part) {
+    __shared__ double red[2 * (kThreads / 64)];
+    float tacc = 0.0f;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
+        float R = 0.0f;
+        for (int g = 0; g < ngroups; ++g) R += rpartial[(size_t)g * MN + q];
+        Rmap[q] = R;
+        const float nn = nrm1[q];
+        if (nn > tau) tacc -= R / nn;
+    }
+    block_sum2(0.0f, tacc, part + 2 * blockIdx.x, red);
+}
+
+// sbar_{k-1} = (2f - 1) wbar + (1 - f) sbar_k + [Nrm > tau] (tau/Nrm^3) R s_{k-1}; g = D^T sbar -> rFFT
+template <int L, int T>
+__global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __restrict__ wbar, const float* __restrict__ sb_in,
+                                                             const float* __restrict__ sk1, const float* __restrict__ nrm1,
+                                                             const float* __restrict__ Rmap, float* __restrict__ sb_out,
+                                                             float2* __restrict__ spec0, const float2* __restrict__ twM,
+                                                             int N, float tau) {
+    constexpr int M = 2 * L;
+    constexpr int M4 = M / 4;
+    constexpr int P = Plan<L>::P;
+    constexpr int RF = plan_radix<L, 0, true>();
+    constexpr int QF = L / RF;
+    constexpr int NE = (T + 1) * M4;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float* W0 = reinterpret_cast<float*>(tw + M);   // sbar ch0, T+1 lines
+    float* W1 = W0 + (T + 1) * M;                   // sbar ch1, T lines
+    float2* F0 = reinterpret_cast<float2*>(W1 + T * M);
+    float2* F1 = F0 + T * L;
+    const int plane = blockIdx.y;
+    const int j0 = blockIdx.x * T;
+    const size_t MN = (size_t)M * N;
+    const int tid = threadIdx.x;
+    const size_t poff = (size_t)plane * 2 * MN;
+    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    for (int idx = tid; idx < NE; idx += kThreads) {
+        const int t = idx / M4, i = (idx - t * M4) * 4;
+        const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+        const float4 nn = *reinterpret_cast<const float4*>(nrm1 + off);
+        const float4 R = *reinterpret_cast<const float4*>(Rmap + off);
+        const float n4[4] = {nn.x, nn.y, nn.z, nn.w}, r4[4] = {R.x, R.y, R.z, R.w};
+        float cf[4], cw[4], cs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float f = bt_factor(n4[q], tau);
+            cw[q] = 2.0f * f - 1.0f;
+            cs[q] = 1.0f - f;
+            cf[q] = n4[q] > tau ? tau / (n4[q] * n4[q] * n4[q]) * r4[q] : 0.0f;
+        }
+        for (int ch = 0; ch < (t < T ? 2 : 1); ++ch) {
+            const size_t o = poff + (size_t)ch * MN + off;
+            const float4 w = *reinterpret_cast<const float4*>(wbar + o);
+            const float4 a = *reinterpret_cast<const float4*>(sk1 + o);
+            float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (sb_in) b = *reinterpret_cast<const float4*>(sb_in + o);
+            float4 r;
+            r.x = cw[0] * w.x + cs[0] * b.x + cf[0] * a.x;
+            r.y = cw[1] * w.y + cs[1] * b.y + cf[1] * a.y;
+            r.z = cw[2] * w.z + cs[2] * b.z + cf[2] * a.z;
+            r.w = cw[3] * w.w + cs[3] * b.w + cf[3] * a.w;
+            *reinterpret_cast<float4*>((ch == 0 ? W0 : W1) + t * M + i) = r;
+            if (t < T) *reinterpret_cast<float4*>(sb_out + o) = r;
+        }
+    }
+    __syncthreads();
+    for (int idx = tid; idx < T * QF; idx += kThreads) {
+        const int f = idx / QF, j = idx - f * QF;
+        float2 v[RF];
+#pragma unroll
+        for (int r = 0; r < RF; ++r) {
+            const int n = j + r * QF;
+            const float2 a = *reinterpret_cast<const float2*>(W0 + f * M + 2 * n);
+            const float2 b = *reinterpret_cast<const float2*>(W0 + (f + 1) * M + 2 * n);
+            const float2 c = *reinterpret_cast<const float2*>(W1 + f * M + 2 * n);
+            const float cn = W1[f * M + ((2 * n + 2) & (M - 1))];
+            v[r].x = (a.x - b.x) + (c.x - c.y);
+            v[r].y = (a.y - b.y) + (c.y - cn);
+        }
+        fly_core<L, RF, 0, false, 2>(v, j, tw);
+        const int o = out_base<L, RF, 0>(j);
+#pragma unroll
+        for (int r = 0; r < RF; ++r) F0[f * L + o + r] = v[r];
+    }
+    __syncthreads();
+    float2* Z;
+    if constexpr (P == 1) {
+        Z = F0;
+    } else if constexpr (P == 2) {
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{F1, L});
+        __syncthreads();
+        Z = F1;
+    } else {
+        plan_pass<L, 1, true, false, 2>(T, tw, LdsIO{F0, L}, LdsIO{F1, L});
+        __syncthreads();
+        plan_pass<L, 2, true, false, 2>(T, tw, LdsIO{F1, L}, LdsIO{F0, L});
+        __syncthreads();
+        Z = F0;
+    }
+    pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
+}
+
 }  // namespace admm

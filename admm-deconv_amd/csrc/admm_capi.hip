@@ -315,6 +315,7 @@ struct Traj {
     float* s = nullptr;      // (K-1) x planes x 2 x M x N : s_k for k = 1..K-1
     float2* v = nullptr;     // K x planes x N x M/2        : forward dim-2 spectra (h_bar only)
     double2* sig = nullptr;  // (M/2+1) x N                 : top-left PSF spectrum (h_bar only)
+    float* nrm = nullptr;    // (K-1) x M x N               : isotropic batch norm of s_k (iso only)
 };
 
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
@@ -406,22 +407,29 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, hty, twM, N, tau, rho, it == 1 ? 1 : 0);
             });
         } else if (it < maxit) {
-            // isotropic: s is written in place (no halo reads of s in ISO_A)
-            float* sa = sbuf[0];
+            // isotropic: s is written in place (no halo reads of s in ISO_A); with a trajectory each
+            // iteration writes its own slot and the batch norm is kept too
+            float* so = sbuf[0];
+            float* sn = sbuf[0];
+            if (tr.s) {
+                so = it >= 2 ? tr.s + (size_t)(it - 2) * sstride : sbuf[0];
+                sn = tr.s + (size_t)(it - 1) * sstride;
+            }
+            float* nrm_out = tr.nrm ? tr.nrm + (size_t)(it - 1) * MN : nullptr;
             const int ng = (int)((np + kIsoGroup - 1) / kIsoGroup);
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, sa, sa, fmap, part, twM, N, (int)np,
+                launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, so, sn, fmap, part, twM, N, (int)np,
                              kIsoGroup, it == 1 ? 1 : 0);
             });
             if (rc) return rc;
             rc = ln.run(ADMM_K_NORM, [&] {
                 const int nb = (int)((MN + kThreads - 1) / kThreads);
                 hipLaunchKernelGGL(admm::iso_r_kernel, dim3(nb < 2048 ? nb : 2048), dim3(kThreads), 0, s, part,
-                                   fmap, ng, MN, tau);
+                                   fmap, ng, MN, tau, nrm_out);
             });
             if (rc) return rc;
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sa, fmap, hty, spec0, twM, N, rho);
+                launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, hty, spec0, twM, N, rho);
             });
         } else {
             rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
@@ -450,12 +458,16 @@ int check_ws(void* workspace, size_t have, size_t need) {
 struct BwdLayout {
     Layout f;
     size_t traj_s, traj_v, sig, sbA, sbB, vsum, rpart, Qp, Q, hpart, hcorr, hA, rt, total;
+    size_t traj_n, wbar, Rmap, Rpart;   // isotropic only
     int nblk_line, nblk_corr, TY;
+    int nblk_isoA, nblk_isoR;           // isotropic: per-step partial rows = nblk_isoA + nblk_isoR
 };
 
-BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h) {
+constexpr int kIsoAdjRBlocks = 256;     // ISO_ADJ_R grid (tau_bar partial rows per step)
+
+BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h, bool iso) {
     BwdLayout b{};
-    b.f = make_layout(M, N, planes, kh > 0, false);
+    b.f = make_layout(M, N, planes, kh > 0, iso);
     size_t off = b.f.total;
     auto take = [&](size_t bytes) {
         size_t o = off;
@@ -472,7 +484,18 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     b.sbA = take(planes * 2 * MN * 4);
     b.sbB = take(planes * 2 * MN * 4);
     b.vsum = take(planes * MN * 4);
-    b.nblk_line = (int)(planes * (N / T));
+    if (iso) {
+        const size_t ng = (planes + kIsoGroup - 1) / kIsoGroup;
+        b.traj_n = take((size_t)(K > 1 ? K - 1 : 1) * MN * 4);
+        b.wbar = take(planes * 2 * MN * 4);
+        b.Rmap = take(MN * 4);
+        b.Rpart = take(ng * MN * 4);
+        b.nblk_isoA = (int)(ng * (N / T));
+        b.nblk_isoR = kIsoAdjRBlocks;
+        b.nblk_line = b.nblk_isoA + b.nblk_isoR;
+    } else {
+        b.nblk_line = (int)(planes * (N / T));
+    }
     b.rpart = take((size_t)K * b.nblk_line * 2 * 8);
     b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 4) : 0;
     b.Q = hq ? take((size_t)(M / 2 + 1) * N * 8) : 0;
@@ -495,6 +518,38 @@ int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
         line_adj_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, part, twM, \
                                                         N, tau, rho, first_k, last_k);                        \
         return 0;                                                                                              \
+    }
+    ADMM_LT_CASES(X)
+#undef X
+    return -1;
+}
+
+int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
+                     const float* sk, const float* xK, const float* nrm1, const float* sb_in, float* wbar, float* vsum,
+                     float* rpartial, double* part, const float2* twM, int N, int planes, int G, float tau, float rho,
+                     int first_k, int last_k) {
+#define X(l, t)                                                                                                 \
+    if (L == l && T == t) {                                                                                     \
+        set_lds(iso_adj_a_kernel<l, t>, lds);                                                                   \
+        iso_adj_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, nrm1, nullptr, sb_in, wbar, vsum,  \
+                                                         rpartial, part, twM, N, planes, G, tau, rho, first_k,  \
+                                                         last_k);                                               \
+        return 0;                                                                                               \
+    }
+    ADMM_LT_CASES(X)
+#undef X
+    return -1;
+}
+
+int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* wbar, const float* sb_in,
+                     const float* sk1, const float* nrm1, const float* Rmap, float* sb_out, float2* spec0,
+                     const float2* twM, int N, float tau) {
+#define X(l, t)                                                                                                 \
+    if (L == l && T == t) {                                                                                     \
+        set_lds(iso_adj_b_kernel<l, t>, lds);                                                                   \
+        iso_adj_b_kernel<l, t><<<g, kThreads, lds, s>>>(wbar, sb_in, sk1, nrm1, Rmap, sb_out, spec0, twM, N,    \
+                                                         tau);                                                  \
+        return 0;                                                                                               \
     }
     ADMM_LT_CASES(X)
 #undef X
@@ -530,9 +585,8 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    if (iso) return fail(ADMM_E_UNSUPPORTED, "backward of the isotropic (BT) prox is not in this build yet");
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
-    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0).total;
+    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
     return ADMM_OK;
 }
 
@@ -543,14 +597,13 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    if (iso) return fail(ADMM_E_UNSUPPORTED, "backward of the isotropic (BT) prox is not in this build yet");
     rc = check_common(y, y_bar, maxit, lambda, rho);
     if (rc) return rc;
     if (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)) return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
     const bool want_h = h_bar != nullptr && kh > 0;
-    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h);
+    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
     unsigned char* ws = static_cast<unsigned char*>(workspace);
@@ -584,7 +637,8 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
     tr.s = reinterpret_cast<float*>(ws + bl.traj_s);
     tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
-    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, 0, K, ws, bl.f, tr);
+    tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
+    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr);
     if (rc) return rc;
     // ---- reverse sweep ----
     float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
@@ -602,6 +656,12 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
     const size_t alds = line_lds(M, T) + 8 * 16;
     const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
     HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
+    float* wbar = iso ? reinterpret_cast<float*>(ws + bl.wbar) : nullptr;
+    float* Rmap = iso ? reinterpret_cast<float*>(ws + bl.Rmap) : nullptr;
+    float* Rpart = iso ? reinterpret_cast<float*>(ws + bl.Rpart) : nullptr;
+    const int ngi = (int)((planes + kIsoGroup - 1) / kIsoGroup);
+    // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
+    if (iso) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
     if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
     rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
     if (rc) return rc;
@@ -616,9 +676,30 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
         const float* sbi = k < K ? sb[k & 1] : nullptr;
         float* sbo = sb[(k & 1) ^ 1];
         double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
+        if (!iso) {
+            rc = ln.run(ADMM_K_LINE, [&] {
+                launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
+                                k == 1 ? 1 : 0, k == K ? 1 : 0);
+            });
+            if (rc) return rc;
+            continue;
+        }
+        // isotropic: ISO_ADJ_A (plane groups) -> ISO_ADJ_R (batch R map, tau_bar) -> ISO_ADJ_B (per plane)
+        const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
         rc = ln.run(ADMM_K_LINE, [&] {
-            launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
-                            k == 1 ? 1 : 0, k == K ? 1 : 0);
+            launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
+                             nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, kIsoGroup, tau, rho,
+                             k == 1 ? 1 : 0, k == K ? 1 : 0);
+        });
+        if (rc) return rc;
+        if (k == 1) break;
+        rc = ln.run(ADMM_K_NORM, [&] {
+            hipLaunchKernelGGL(admm::iso_adj_r_kernel, dim3(kIsoAdjRBlocks), dim3(kThreads), 0, s, Rpart, Rmap, nrm1,
+                               ngi, MN, tau, rp + (size_t)bl.nblk_isoA * 2);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_LINE, [&] {
+            launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau);
         });
         if (rc) return rc;
     }

@@ -692,12 +692,15 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
     }
 }
 
+// nrm_out (optional) keeps the per-pixel batch norm for the adjoint (trajectory recording)
 __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
-                                                         int ngroups, size_t MN, float tau) {
+                                                         int ngroups, size_t MN, float tau, float* __restrict__ nrm_out) {
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
         float acc = 0.0f;
         for (int g = 0; g < ngroups; ++g) acc += part[(size_t)g * MN + q];
-        fmap[q] = max0_nan(1.0f - tau / sqrtf(acc));   // BT factor, ops.jl:10
+        const float nrm = sqrtf(acc);
+        fmap[q] = max0_nan(1.0f - tau / nrm);   // BT factor, ops.jl:10
+        if (nrm_out) nrm_out[q] = nrm;
     }
 }
 

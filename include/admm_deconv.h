@@ -81,7 +81,9 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
  * runs the reverse sweep.  Given x_bar = dL/dx it writes
  *   y_bar (device, shape of y)   h_bar (device, kw*kh floats; NULL = not needed, cheaper)
  *   lambda_bar, rho_bar (device, 1 float each; NULL = not needed)
- * Anisotropic prox only in this build (iso != 0 returns ADMM_E_UNSUPPORTED).  Deterministic. */
+ * Both proxes: with iso != 0 the trajectory also keeps the per-pixel batch norm of every s_k and
+ * each reverse step reduces R = sum over planes of s (2 w_bar - s_bar) across the batch.
+ * Deterministic (fixed reduction order). */
 int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso, int maxit,
                                       int want_hbar, size_t* out_bytes);
 int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,

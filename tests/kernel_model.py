@@ -132,8 +132,14 @@ def _Dt(a, b):
     return (a - np.roll(a, -1, axis=-2)) + (b - np.roll(b, -1, axis=-1))
 
 
-def tvd_model_grads(y_c, lam, rho, h_c, K, xbar):
-    """y_c (planes, N, M); returns (x, ybar, hbar, lam_bar, rho_bar) following the kernel reverse sweep."""
+def tvd_model_grads(y_c, lam, rho, h_c, K, xbar, iso=False):
+    """y_c (planes, N, M); returns (x, ybar, hbar, lam_bar, rho_bar) following the kernel reverse sweep.
+
+    iso: the BT prox z = f s, f = max(1 - tau/Nrm, 0), Nrm(pixel) = sqrt(sum over all planes and both
+    channels of s^2) (ops.jl:6,10).  Then w = phi(s) = (2f-1) s, u = psi(s) = (1-f) s, and the reverse
+    step gains a per-pixel batch reduction R = sum_{planes,channels} s (2 wbar - sbar):
+        sbar_{k-1} = (2f-1) wbar + (1-f) sbar_k + [Nrm > tau] (tau/Nrm^3) R s
+        tau_bar   += sum_pixels [Nrm > tau] (-R/Nrm)."""
     y = np.asarray(y_c, np.float64)
     Pl, N, M = y.shape
     tau = lam / rho
@@ -149,10 +155,26 @@ def tvd_model_grads(y_c, lam, rho, h_c, K, xbar):
         S = sum(h_c[b, a] * np.exp(-2j * np.pi * (a * k / M + b * kj / N)) for b in range(kw) for a in range(kh))
     Cf = 1.0 / (np.abs(S) ** 2 + rho * lapf)
     Ainv = lambda v: np.real(np.fft.ifft2(Cf * np.fft.fft2(v)))   # noqa: E731
-    phi = lambda s: np.where(np.abs(s) > tau, s - 2 * tau * np.sign(s), -s)   # noqa: E731
-    psi = lambda s: np.clip(s, -tau, tau)   # noqa: E731
+
+    def fmap(sk):
+        with np.errstate(divide="ignore"):
+            nrm = np.sqrt(np.sum(sk * sk, axis=(0, 1)))
+            return np.maximum(1 - tau / nrm, 0.0), nrm
+
+    def phi(sk, f=None):
+        if iso:
+            return (2 * f - 1) * sk
+        return np.where(np.abs(sk) > tau, sk - 2 * tau * np.sign(sk), -sk)
+
+    def psi(sk, f=None):
+        if iso:
+            return (1 - f) * sk
+        return np.clip(sk, -tau, tau)
+
     # forward with trajectory
     s = [np.zeros((2, Pl, N, M))]
+    fs = [np.zeros((N, M))]
+    nrms = [np.zeros((N, M))]
     vs = []
     w = np.zeros((2, Pl, N, M))
     u = np.zeros((2, Pl, N, M))
@@ -164,8 +186,11 @@ def tvd_model_grads(y_c, lam, rho, h_c, K, xbar):
             break
         d0, d1 = _Dop(x)
         sk = np.stack([d0 + u[0], d1 + u[1]])
+        f, nrm = fmap(sk) if iso else (None, None)
         s.append(sk)
-        w, u = phi(sk), psi(sk)
+        fs.append(f)
+        nrms.append(nrm)
+        w, u = phi(sk, f), psi(sk, f)
     xK = x
     # reverse sweep
     g = np.asarray(xbar, np.float64).reshape(Pl, N, M)
@@ -181,15 +206,26 @@ def tvd_model_grads(y_c, lam, rho, h_c, K, xbar):
         if it == K:
             dx0, dx1 = _Dop(xK)
         else:
-            dx0, dx1 = s[it][0] - psi(s[it - 1][0]), s[it][1] - psi(s[it - 1][1])
+            up = psi(s[it - 1], fs[it - 1])
+            dx0, dx1 = s[it][0] - up[0], s[it][1] - up[1]
         rho_bar -= np.sum(dv0 * dx0 + dv1 * dx1)
         if it >= 2:
             sp = s[it - 1]
-            wb = rho * np.stack([dv0, dv1])
-            rho_bar += np.sum(phi(sp) * np.stack([dv0, dv1]))
-            m = np.abs(sp) > tau
-            sbar_new = np.where(m, wb, -wb + sbar)
-            tau_bar += np.sum(np.where(m, -2 * np.sign(sp) * wb + np.sign(sp) * sbar, 0.0))
+            dv = np.stack([dv0, dv1])
+            wb = rho * dv
+            rho_bar += np.sum(phi(sp, fs[it - 1]) * dv)
+            if iso:
+                f, nrm = fs[it - 1], nrms[it - 1]
+                R = np.sum(sp * (2 * wb - sbar), axis=(0, 1))
+                act = nrm > tau
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    coef = np.where(act, tau / nrm ** 3 * R, 0.0)
+                    tau_bar += np.sum(np.where(act, -R / nrm, 0.0))
+                sbar_new = (2 * f - 1) * wb + (1 - f) * sbar + coef * sp
+            else:
+                m = np.abs(sp) > tau
+                sbar_new = np.where(m, wb, -wb + sbar)
+                tau_bar += np.sum(np.where(m, -2 * np.sign(sp) * wb + np.sign(sp) * sbar, 0.0))
             sbar = sbar_new
             g = _Dt(sbar[0], sbar[1])
     # final assembly

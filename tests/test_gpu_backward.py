@@ -77,6 +77,39 @@ def test_backward_vs_autograd(dev, case):
         assert np.linalg.norm(hb - hb0) / np.linalg.norm(hb0) < stol
 
 
+ISO_CASES = [
+    # (B, P, N, M, psf, lam, rho, K, scalar_tol) -- isotropic (BT) prox: the batch norm couples all planes;
+    # 20 planes span two ISO_ADJ_A plane groups (16 planes per group)
+    (20, 1, 32, 32, ("gauss", 5, 1.0), 0.02, 0.1, 6, 1e-3),
+    (2, 3, 64, 64, ("rand", 7, 4), 0.0041, 0.021, 10, 1e-3),
+    (3, 1, 64, 128, None, 0.05, 0.02, 8, 1e-3),
+    (1, 1, 16, 32, ("gauss", 3, 0.8), 0.02, 0.1, 1, 1e-3),
+    (2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, 1e-2),
+]
+
+
+@pytest.mark.parametrize("case", ISO_CASES, ids=[f"iso-{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}" for c in ISO_CASES])
+def test_backward_iso_vs_autograd(dev, case):
+    B, P, N, M, spec, lam, rho, K, stol = case
+    rng = np.random.default_rng(7 * N + M + K)
+    h = psf(spec, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=5)
+    xbar = rng.standard_normal(y.shape).astype(np.float32)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev),
+                                                     lam, rho, ht, True, K)
+    torch.cuda.synchronize()
+    x0, yb0, hb0, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
+                                                        None if h is None else h.astype(np.float64), True, K, xbar)
+    assert_parity(x.cpu().numpy(), x0, what="x")
+    assert_grad(yb.cpu().numpy(), yb0, "y_bar")
+    assert rel(float(lb), lb0) < stol, (float(lb), lb0)
+    assert rel(float(rb), rb0) < stol, (float(rb), rb0)
+    if h is not None:
+        hb = hb.cpu().numpy()
+        assert np.linalg.norm(hb - hb0) / np.linalg.norm(hb0) < stol
+
+
 def test_autograd_function_and_layer_grads(dev):
     """torch.autograd through tvd_fft and through a layer (the rrule path), against the oracle."""
     from admm_deconv import layers
@@ -98,13 +131,14 @@ def test_autograd_function_and_layer_grads(dev):
     assert rel(float(L.lam.grad), lb0) < 1e-3 and rel(float(L.rho.grad), rb0) < 1e-3
 
 
-def test_backward_deterministic(dev):
+@pytest.mark.parametrize("iso", [False, True])
+def test_backward_deterministic(dev, iso):
     h = synth.gaussian_psf(9, 1.5)
     y = torch.from_numpy(synth.make_batch(3, 64, 64, h)).to(dev)
     xb = torch.randn_like(y)
     ht = torch.from_numpy(h).to(dev)
-    a = admm_deconv.tvd_fft_backward(y, xb, 0.01, 0.05, ht, False, 7)
-    b = admm_deconv.tvd_fft_backward(y, xb, 0.01, 0.05, ht, False, 7)
+    a = admm_deconv.tvd_fft_backward(y, xb, 0.01, 0.05, ht, iso, 7)
+    b = admm_deconv.tvd_fft_backward(y, xb, 0.01, 0.05, ht, iso, 7)
     torch.cuda.synchronize()
     for u, v in zip(a, b):
         assert torch.equal(u, v)
