@@ -16,6 +16,7 @@ ADMM_E_INVALID = -1
 ADMM_E_UNSUPPORTED = -2
 ADMM_E_WORKSPACE = -3
 ADMM_E_HIP = -4
+ADMM_E_REDUCER = -5
 
 K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE = range(7)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
@@ -24,7 +25,16 @@ KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: 
 # Every symbol include/admm_deconv.h declares (checked by tests/test_capi.py).
 EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "admm_tvd_forward_f32",
            "admm_tvd_backward_workspace_bytes", "admm_tvd_backward_f32",
+           "admm_tvd_forward_sharded_f32", "admm_tvd_backward_sharded_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
+
+
+# admm_reduce_fn / admm_batch_reducer (include/admm_deconv.h): cross-shard sum of an M x N map
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class BatchReducer(ctypes.Structure):
+    _fields_ = [("fn", REDUCE_FN), ("user", ctypes.c_void_p)]
 
 
 class AdmmError(RuntimeError):
@@ -65,6 +75,10 @@ def load():
     L.admm_tvd_backward_f32.argtypes = [c_void_p] * 6 + [c_int] * 4 + [c_void_p, c_int, c_int, c_float, c_float,
                                                                          c_int, c_int, c_void_p, c_void_p, c_size_t,
                                                                          c_void_p]
+    L.admm_tvd_forward_sharded_f32.restype = c_int
+    L.admm_tvd_forward_sharded_f32.argtypes = list(L.admm_tvd_forward_f32.argtypes) + [ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_backward_sharded_f32.restype = c_int
+    L.admm_tvd_backward_sharded_f32.argtypes = list(L.admm_tvd_backward_f32.argtypes) + [ctypes.POINTER(BatchReducer)]
     L.admm_profile_enable.restype = c_int
     L.admm_profile_enable.argtypes = [c_int]
     L.admm_profile_reset.restype = c_int

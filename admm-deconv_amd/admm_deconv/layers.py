@@ -78,6 +78,9 @@ class Admm:
         self.iters = int(iters)
         self.iso = bool(iso)
         self.creg = float(creg)
+        # torch.distributed group the batch is sharded over (isotropic prox: the pixelnorm spans the
+        # whole sharded batch, see ops.tvd_fft); None = this process holds the whole batch
+        self.group = None
 
     # Flux.@layer ... trainable=(...)
     def trainable(self):
@@ -110,7 +113,7 @@ class Admm:
             self.rho.clamp_(min=self.creg)                       # :217
             self.weight.clamp_(0.0, 1.0)                         # :219
         h = self.weight if self.weight.numel() > 0 else None
-        res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters)   # :221
+        res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters, group=self.group)   # :221
         if self.bias is not False:
             res = res + self.bias                                 # :222
         return self.sigma(res)                                    # :224

@@ -11,6 +11,8 @@ reference's Julia array (M, N, P, B).  The PSF h is torch (kw, kh) == Julia (kh,
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
 import math
 
 import torch
@@ -37,6 +39,45 @@ class Workspace:
 _default_ws = {}
 
 
+def _make_reducer(workspace, group):
+    """admm_batch_reducer for a batch sharded over `group` (isotropic prox; include/admm_deconv.h).
+
+    The library hands over a device pointer into `workspace` holding this shard's M x N partial map;
+    the callback all-reduces (sum) that slice of the workspace tensor in place, on the library's
+    stream.  gloo (CPU-only collectives) goes through a host copy.  Returns (struct, keep-alive)."""
+    import torch.distributed as dist
+
+    def cb(buf, count, stream, _user):
+        try:
+            base = workspace._buf.data_ptr()
+            off = int(buf) - base
+            view = workspace._buf[off: off + 4 * int(count)].view(torch.float32)
+            on_dev = (torch.cuda.stream(torch.cuda.ExternalStream(int(stream or 0), device=view.device))
+                      if view.is_cuda else contextlib.nullcontext())
+            with on_dev:
+                if dist.get_backend(group) == "gloo":
+                    host = view.cpu()
+                    dist.all_reduce(host, group=group)
+                    view.copy_(host)
+                else:
+                    dist.all_reduce(view, group=group)
+            return 0
+        except BaseException as e:   # an exception must not unwind through the C frames
+            import sys
+            print(f"admm_deconv batch reducer failed: {e!r}", file=sys.stderr)
+            return -1
+
+    fn = _lib.REDUCE_FN(cb)
+    return _lib.BatchReducer(fn, None), fn
+
+
+def _sharded(isotropic, group):
+    if group is None or not isotropic:
+        return False
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_world_size(group) > 1
+
+
 def _scalar(v, name):
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
@@ -52,7 +93,8 @@ def _scalar(v, name):
     return v
 
 
-def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None):
+def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None,
+                 group=None):
     """ADMM TV deconvolution of every (M x N) plane of y (ops.jl:181).
 
     y:    torch float32 tensor (B, P, N, M) on a ROCm device (Julia (M,N,P,B)); a 2-D (N, M) or
@@ -99,9 +141,16 @@ def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=Non
     if stream is None:
         stream = torch.cuda.current_stream(y.device)
     s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
-    _lib.check(_lib.load().admm_tvd_forward_f32(
-        y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, int(bool(isotropic)), int(maxit),
-        ws_ptr, ws_len, s_handle))
+    if _sharded(isotropic, group):
+        red, keep = _make_reducer(workspace, group)
+        _lib.check(_lib.load().admm_tvd_forward_sharded_f32(
+            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, 1, int(maxit),
+            ws_ptr, ws_len, s_handle, ctypes.byref(red)))
+        del keep
+    else:
+        _lib.check(_lib.load().admm_tvd_forward_f32(
+            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, int(bool(isotropic)), int(maxit),
+            ws_ptr, ws_len, s_handle))
     return out.reshape(shape)
 
 
@@ -119,10 +168,12 @@ def _prep(y, h):
 
 
 def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, workspace=None,
-                     stream=None):
+                     stream=None, group=None):
     """Adjoint of tvd_fft through all `maxit` unrolled iterations (what Zygote computes for the
     reference, src/train.jl:51).  Returns (x, y_bar, h_bar, lam_bar, rho_bar); h_bar is None without a PSF
-    or when need_h is False.  Recomputes the forward (x is returned for convenience)."""
+    or when need_h is False.  Recomputes the forward (x is returned for convenience).
+    With `group` (isotropic prox, batch sharded over the group's ranks) h_bar / lam_bar / rho_bar are
+    this shard's contributions: their sum over ranks is the gradient of the whole batch."""
     shape, y4, hb = _prep(y, h)
     B, P, N, M = y4.shape
     xb = x_bar.reshape(y4.shape).to(torch.float32).contiguous()
@@ -141,10 +192,15 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     y_bar = torch.empty_like(y4)
     h_bar = torch.empty_like(hb) if want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y.device)
-    _lib.check(_lib.load().admm_tvd_backward_f32(
-        y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
-        scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, lam, rho,
-        int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle))
+    args = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
+            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, lam, rho,
+            int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle)
+    if _sharded(isotropic, group):
+        red, keep = _make_reducer(workspace, group)
+        _lib.check(_lib.load().admm_tvd_backward_sharded_f32(*args, ctypes.byref(red)))
+        del keep
+    else:
+        _lib.check(_lib.load().admm_tvd_backward_f32(*args))
     return x.reshape(shape), y_bar.reshape(shape), h_bar, scal[0], scal[1]
 
 
@@ -153,37 +209,42 @@ class _TvdFFTFn(torch.autograd.Function):
     (the rrule the Julia shim would register, julia/ADMMDeconvHIP.jl)."""
 
     @staticmethod
-    def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit):
+    def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit, group):
         ctx.save_for_backward(y, lam_t, rho_t, h_t)
-        ctx.iso, ctx.maxit = isotropic, maxit
-        return _forward_raw(y, lam_t, rho_t, h_t, isotropic, maxit)
+        ctx.iso, ctx.maxit, ctx.group = isotropic, maxit, group
+        return _forward_raw(y, lam_t, rho_t, h_t, isotropic, maxit, group=group)
 
     @staticmethod
     def backward(ctx, x_bar):
         y, lam_t, rho_t, h_t = ctx.saved_tensors
         need_h = h_t is not None and h_t.numel() > 0 and ctx.needs_input_grad[3]
         _, yb, hb, lb, rb = tvd_fft_backward(y, x_bar, lam_t, rho_t, h_t if h_t.numel() else None, ctx.iso,
-                                             ctx.maxit, need_h=need_h)
+                                             ctx.maxit, need_h=need_h, group=ctx.group)
         hg = None
         if need_h:
             hg = hb.reshape(h_t.shape)
         return (yb if ctx.needs_input_grad[0] else None,
                 lb.reshape(lam_t.shape).to(lam_t.dtype) if ctx.needs_input_grad[1] else None,
                 rb.reshape(rho_t.shape).to(rho_t.dtype) if ctx.needs_input_grad[2] else None,
-                hg, None, None)
+                hg, None, None, None)
 
 
-def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None):
+def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None,
+            group=None):
     """ADMM TV deconvolution of every (M x N) plane of y -- src/ops/ops.jl:181 semantics.
 
     y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: scalars or
     1-element tensors; h: PSF (kw,kh) (= Julia (kh,kw)) or None/empty.  Returns a new tensor.
     Differentiable (y, lam, rho, h) when autograd is recording and any of them requires grad
-    (either prox); the gradient is the exact adjoint of the K unrolled iterations."""
+    (either prox); the gradient is the exact adjoint of the K unrolled iterations.
+    group: torch.distributed group the batch is sharded over (each rank passes its own slice).  The
+    isotropic prox's pixelnorm then spans the whole sharded batch (one M x N all-reduce per
+    iteration), so every rank gets its slice of the unsharded result; ignored for the anisotropic
+    prox, whose planes are independent."""
     tensors = [t for t in (y, lam, rho, h) if isinstance(t, torch.Tensor)]
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
         dev = y.device
         as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.tensor([float(v)], device=dev)  # noqa: E731
         h_t = h if isinstance(h, torch.Tensor) else torch.zeros(0, device=dev)
-        return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit))
-    return _forward_raw(y, lam, rho, h, isotropic, maxit, out=out, workspace=workspace, stream=stream)
+        return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit), group)
+    return _forward_raw(y, lam, rho, h, isotropic, maxit, out=out, workspace=workspace, stream=stream, group=group)

@@ -320,9 +320,16 @@ struct Traj {
 
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
 // Returns the Launcher's status; `ln` keeps the events for the profiler.
+// the caller's cross-shard sum of an M x N map (isotropic prox over a sharded batch)
+int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStream_t s) {
+    const int r = red->fn(buf, count, reinterpret_cast<void*>(s), red->user);
+    if (r != 0) return fail(ADMM_E_REDUCER, "batch reducer returned %d", r);
+    return ADMM_OK;
+}
+
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
                 int kw, float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                const Traj& tr) {
+                const Traj& tr, const admm_batch_reducer* red) {
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
     const size_t MN = (size_t)M * N;
@@ -422,11 +429,24 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                              kIsoGroup, it == 1 ? 1 : 0);
             });
             if (rc) return rc;
-            rc = ln.run(ADMM_K_NORM, [&] {
-                const int nb = (int)((MN + kThreads - 1) / kThreads);
-                hipLaunchKernelGGL(admm::iso_r_kernel, dim3(nb < 2048 ? nb : 2048), dim3(kThreads), 0, s, part,
-                                   fmap, ng, MN, tau, nrm_out);
-            });
+            const int nb = (int)((MN + kThreads - 1) / kThreads);
+            const dim3 gr(nb < 2048 ? nb : 2048);
+            if (red) {
+                // sharded batch: per-shard sum -> caller's all-reduce -> BT factor
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    hipLaunchKernelGGL(admm::iso_sum_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN);
+                });
+                if (rc) return rc;
+                rc = call_reducer(red, fmap, MN, s);
+                if (rc) return rc;
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, nrm_out);
+                });
+            } else {
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, nrm_out);
+                });
+            }
             if (rc) return rc;
             rc = ln.run(ADMM_K_LINE, [&] {
                 launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, hty, spec0, twM, N, rho);
@@ -563,6 +583,14 @@ extern "C" {
 int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
                          float lambda, float rho, int iso, int maxit, void* workspace, size_t workspace_bytes,
                          void* stream) {
+    return admm_tvd_forward_sharded_f32(y, x_out, M, N, P, B, h, kh, kw, lambda, rho, iso, maxit, workspace,
+                                        workspace_bytes, stream, nullptr);
+}
+
+int admm_tvd_forward_sharded_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
+                                 int kw, float lambda, float rho, int iso, int maxit, void* workspace,
+                                 size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    const admm_batch_reducer* red = (iso && reducer && reducer->fn) ? reducer : nullptr;
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
@@ -575,7 +603,7 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
     if (rc) return rc;
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
     rc = run_forward(ln, y, x_out, M, N, planes, h, kh, kw, lambda, rho, iso, maxit,
-                     static_cast<unsigned char*>(workspace), lay, Traj{});
+                     static_cast<unsigned char*>(workspace), lay, Traj{}, red);
     int rc2 = ln.finish();
     return rc ? rc : rc2;
 }
@@ -594,6 +622,15 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
                           float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw, float lambda,
                           float rho, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
                           void* stream) {
+    return admm_tvd_backward_sharded_f32(y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda,
+                                         rho, iso, maxit, x_out, workspace, workspace_bytes, stream, nullptr);
+}
+
+int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                                  float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                                  float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
+                                  size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    const admm_batch_reducer* red = (iso && reducer && reducer->fn) ? reducer : nullptr;
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
@@ -638,7 +675,7 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
     tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
-    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr);
+    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr, red);
     if (rc) return rc;
     // ---- reverse sweep ----
     float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
@@ -698,6 +735,12 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
                                ngi, MN, tau, rp + (size_t)bl.nblk_isoA * 2);
         });
         if (rc) return rc;
+        // sharded batch: tau_bar above used this shard's R (shard contributions add up, like every other
+        // parameter gradient); sbar needs the whole batch's R
+        if (red) {
+            rc = call_reducer(red, Rmap, MN, s);
+            if (rc) return rc;
+        }
         rc = ln.run(ADMM_K_LINE, [&] {
             launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau);
         });

@@ -704,6 +704,26 @@ __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict
     }
 }
 
+// sharded batch (admm_batch_reducer): ISO_R splits into the per-shard sum, the caller's cross-shard
+// all-reduce of that M x N map, and the BT factor
+__global__ __launch_bounds__(kThreads) void iso_sum_kernel(const float* __restrict__ part, float* __restrict__ acc,
+                                                           int ngroups, size_t MN) {
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
+        float a = 0.0f;
+        for (int g = 0; g < ngroups; ++g) a += part[(size_t)g * MN + q];
+        acc[q] = a;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ fmap, size_t MN, float tau,
+                                                           float* __restrict__ nrm_out) {
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
+        const float nrm = sqrtf(fmap[q]);   // fmap holds the all-reduced sum of squares
+        fmap[q] = max0_nan(1.0f - tau / nrm);
+        if (nrm_out) nrm_out[q] = nrm;
+    }
+}
+
 template <int L, int T>
 __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict__ s_new, const float* __restrict__ fmap,
                                                          const float* __restrict__ hty, float2* __restrict__ spec0,

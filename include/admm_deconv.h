@@ -40,7 +40,8 @@ enum {
     ADMM_E_INVALID = -1,      /* bad argument (null pointer, negative size, non-finite λ/ρ) */
     ADMM_E_UNSUPPORTED = -2,  /* shape/option outside this build's support matrix           */
     ADMM_E_WORKSPACE = -3,    /* workspace too small or misaligned                          */
-    ADMM_E_HIP = -4           /* a HIP runtime call failed (message has hipGetErrorString)   */
+    ADMM_E_HIP = -4,          /* a HIP runtime call failed (message has hipGetErrorString)   */
+    ADMM_E_REDUCER = -5       /* the caller's batch reducer (admm_batch_reducer) failed       */
 };
 
 /* Kernel classes, for the optional per-kernel profiler (admm_profile_*). */
@@ -90,6 +91,37 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
                           float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
                           const float* h, int kh, int kw, float lambda, float rho, int iso, int maxit,
                           float* x_out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Sharded batch for the isotropic prox.  BT's pixelnorm sums s^2 over EVERY plane of
+ * the batch (ops.jl:6), so when the batch is split across processes (one per GPU) each iteration
+ * needs the cross-shard sum of one M x N fp32 map.  The library calls
+ *     fn(buf, count, stream, user)
+ * with `buf` a device pointer into the workspace holding this shard's `count` = M*N partial sums;
+ * fn must replace them, in place, by the element-wise sum over all shards, ordered after the work
+ * already enqueued on `stream` and before work enqueued on `stream` after it returns (an
+ * ncclAllReduce(sum) on `stream`, or torch.distributed.all_reduce on the stream's torch twin).
+ * Every shard must make the same sequence of calls.  fn returns 0 on success; a non-zero return
+ * aborts the solve with ADMM_E_REDUCER.  The forward calls it K-1 times (pixelnorm of s_1..s_{K-1});
+ * the backward K-1 times more (the batch map R of each reverse step).  Backward outputs are this
+ * shard's: y_bar for its planes, and its CONTRIBUTION to h_bar / lambda_bar / rho_bar (sum them over
+ * shards, as data-parallel training all-reduces every parameter gradient).
+ * With iso == 0 the reducer is ignored (planes are independent).  reducer == NULL (or fn == NULL)
+ * is the unsharded call, identical to admm_tvd_forward_f32 / admm_tvd_backward_f32. */
+typedef int (*admm_reduce_fn)(float* buf, size_t count, void* stream, void* user);
+typedef struct {
+    admm_reduce_fn fn;
+    void* user;
+} admm_batch_reducer;
+
+int admm_tvd_forward_sharded_f32(const float* y, float* x_out, int M, int N, int P, int B,
+                                 const float* h, int kh, int kw, float lambda, float rho, int iso,
+                                 int maxit, void* workspace, size_t workspace_bytes, void* stream,
+                                 const admm_batch_reducer* reducer);
+int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                                  float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
+                                  const float* h, int kh, int kw, float lambda, float rho, int iso,
+                                  int maxit, float* x_out, void* workspace, size_t workspace_bytes,
+                                  void* stream, const admm_batch_reducer* reducer);
 
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises

@@ -132,14 +132,18 @@ def _Dt(a, b):
     return (a - np.roll(a, -1, axis=-2)) + (b - np.roll(b, -1, axis=-1))
 
 
-def tvd_model_grads(y_c, lam, rho, h_c, K, xbar, iso=False):
+def tvd_model_grads(y_c, lam, rho, h_c, K, xbar, iso=False, batch_sum=None):
     """y_c (planes, N, M); returns (x, ybar, hbar, lam_bar, rho_bar) following the kernel reverse sweep.
 
     iso: the BT prox z = f s, f = max(1 - tau/Nrm, 0), Nrm(pixel) = sqrt(sum over all planes and both
     channels of s^2) (ops.jl:6,10).  Then w = phi(s) = (2f-1) s, u = psi(s) = (1-f) s, and the reverse
     step gains a per-pixel batch reduction R = sum_{planes,channels} s (2 wbar - sbar):
         sbar_{k-1} = (2f-1) wbar + (1-f) sbar_k + [Nrm > tau] (tau/Nrm^3) R s
-        tau_bar   += sum_pixels [Nrm > tau] (-R/Nrm)."""
+        tau_bar   += sum_pixels [Nrm > tau] (-R/Nrm).
+    batch_sum: for a batch sharded over processes, maps this shard's (N, M) per-pixel partial sum to the
+    whole batch's (the admm_batch_reducer contract); tau_bar then uses the shard's own R, so the
+    scalar gradients are this shard's contributions."""
+    batch_sum = batch_sum or (lambda a: a)
     y = np.asarray(y_c, np.float64)
     Pl, N, M = y.shape
     tau = lam / rho
@@ -158,7 +162,7 @@ def tvd_model_grads(y_c, lam, rho, h_c, K, xbar, iso=False):
 
     def fmap(sk):
         with np.errstate(divide="ignore"):
-            nrm = np.sqrt(np.sum(sk * sk, axis=(0, 1)))
+            nrm = np.sqrt(batch_sum(np.sum(sk * sk, axis=(0, 1))))
             return np.maximum(1 - tau / nrm, 0.0), nrm
 
     def phi(sk, f=None):
@@ -219,8 +223,9 @@ def tvd_model_grads(y_c, lam, rho, h_c, K, xbar, iso=False):
                 R = np.sum(sp * (2 * wb - sbar), axis=(0, 1))
                 act = nrm > tau
                 with np.errstate(divide="ignore", invalid="ignore"):
-                    coef = np.where(act, tau / nrm ** 3 * R, 0.0)
                     tau_bar += np.sum(np.where(act, -R / nrm, 0.0))
+                    R = batch_sum(R)
+                    coef = np.where(act, tau / nrm ** 3 * R, 0.0)
                 sbar_new = (2 * f - 1) * wb + (1 - f) * sbar + coef * sp
             else:
                 m = np.abs(sp) > tau
