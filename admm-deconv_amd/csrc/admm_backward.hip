@@ -74,8 +74,9 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
     float2* Bf = X + TH * L;
     float2* Cf = Bf + TH * L;
     double* red = reinterpret_cast<double*>(Cf + TH * L);   // 2 doubles per wave
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const size_t poff = (size_t)plane * 2 * MN;
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
             }
         }
     }
-    block_sum2(rho_acc, tau_acc, part + 2 * ((size_t)plane * gridDim.x + blockIdx.x), red);
+    block_sum2(rho_acc, tau_acc, part + 2 * ((size_t)plane * gridDim.x + xb.x), red);
     if (first_k) return;   // k = 1: no g_0 (block-uniform)
     __syncthreads();
     // ---- g_{k-1} = D^T sbar_{k-1}, fed straight into the forward pass 0 along dim 1 ----
@@ -376,8 +377,9 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
     float2* Bf = X + TH * L;
     float2* Cf = Bf + TH * L;
     double* red = reinterpret_cast<double*>(Cf + TH * L);
-    const int j0 = blockIdx.x * T;
-    const int grp = blockIdx.y;
+    const XBlk xb = xcd_block();
+    const int j0 = xb.x * T;
+    const int grp = xb.y;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
         }
     }
     __syncthreads();
-    block_sum2(rho_acc, 0.0f, part + 2 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x), red);
+    block_sum2(rho_acc, 0.0f, part + 2 * ((size_t)grp * gridDim.x + xb.x), red);
 }
 
 // R map = sum over plane groups of the partial sums; tau_bar partials (block-reduced, one pair per block)
@@ -535,8 +537,9 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
     float* W1 = W0 + (T + 1) * M;                   // sbar ch1, T lines
     float2* F0 = reinterpret_cast<float2*>(W1 + T * M);
     float2* F1 = F0 + T * L;
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const size_t poff = (size_t)plane * 2 * MN;

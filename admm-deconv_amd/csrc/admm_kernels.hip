@@ -34,6 +34,25 @@ namespace admm {
 
 constexpr int kThreads = 256;
 
+// XCD-aware block order (2-D grid (x, y) -> logical (x, y)).  Workgroups are dealt round-robin over
+// the 8 XCDs, each with its own L2 (MI355X_MICROARCH.md, workgroup dispatch): the bijective remap
+// gives each XCD a contiguous run of logical blocks, so neighbours that share cache lines (column
+// slots 32 B apart at N = 512, the halo lines of line tiles) hit the same L2.  Speed only.
+struct XBlk {
+    int x, y;
+};
+__device__ __forceinline__ XBlk xcd_block() {
+#ifdef ADMM_NO_XCD_SWIZZLE
+    return {(int)blockIdx.x, (int)blockIdx.y};
+#else
+    const unsigned nx = gridDim.x, n = nx * gridDim.y;
+    const unsigned orig = blockIdx.x + nx * blockIdx.y;
+    const unsigned q = n / 8, r = n % 8, g = orig % 8;
+    const unsigned id = (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + orig / 8;
+    return {(int)(id % nx), (int)(id / nx)};
+#endif
+}
+
 // ----------------------------------------------------------------------------------------------
 // setup: twiddle tables and multiplier tables, built in fp64 (ops.jl:22-37)
 //   Ct[kj][k] = 1/(MN) / (|Sigma|^2 + rho(|Lx|^2 + |Ly|^2))     k = 0..M/2  (transposed: k fastest)
@@ -174,8 +193,9 @@ __global__ __launch_bounds__(kThreads) void line_fwd_kernel(const float* __restr
     float2* tw = reinterpret_cast<float2*>(smem_raw);
     float2* X = tw + M;
     float2* Bf = X + T * L;
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
     __syncthreads();
     const float2* sp = reinterpret_cast<const float2*>(src + (size_t)plane * N * M);
@@ -197,8 +217,9 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
     float2* tw = reinterpret_cast<float2*>(smem_raw);
     float2* X = tw + M;
     float2* Bf = X + T * L;
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
     load_lines<L>(spec + (size_t)plane * N * L, X, j0, T, N);
     __syncthreads();
@@ -233,8 +254,9 @@ __global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, flo
     float2* tw = reinterpret_cast<float2*>(smem_raw);
     float2* S0 = tw + NN;        // slot-0 spectrum for the mirror term
     float2* buf = S0 + NN;
-    const int plane = blockIdx.y;
-    const int k0 = blockIdx.x * KB;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int k0 = xb.x * KB;
     const int H = L + 1;
     const float2* gsrc = src + (size_t)plane * NN * L + k0;
     float2* gdst = dst + (size_t)plane * NN * L + k0;
@@ -433,8 +455,9 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     float2* X = tw + M;           // TH lines
     float2* Bf = X + TH * L;      // TH lines
     float2* Cf = Bf + TH * L;     // TH lines (w1; 3rd ping-pong buffer for 3-pass plans)
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const float* so = s_old + (size_t)plane * 2 * MN;
@@ -608,8 +631,9 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
     float2* X = tw + M;
     float2* Bf = X + TH * L;
     float2* Cf = Bf + TH * L;
-    const int j0 = blockIdx.x * T;
-    const int grp = blockIdx.y;
+    const XBlk xb = xcd_block();
+    const int j0 = xb.x * T;
+    const int grp = xb.y;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
@@ -740,8 +764,9 @@ __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict
     float* W1 = W0 + (T + 1) * M;                   // T lines
     float2* F0 = reinterpret_cast<float2*>(W1 + T * M);   // T lines
     float2* F1 = F0 + T * L;                               // T lines
-    const int plane = blockIdx.y;
-    const int j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();
+    const int plane = xb.y;
+    const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const float* sp = s_new + (size_t)plane * 2 * MN;

@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic images generated per rank (tiled)")
+    ap.add_argument("--iso", action="store_true",
+                    help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
     return ap.parse_args()
 
 
@@ -90,7 +92,8 @@ def bench_c5(args, dev):
     cfg = synth.CONFIGS["c5"]
     M, N, P, B, K = cfg["M"], cfg["N"], cfg["P"], args.batch or cfg["B"], cfg["K"]
     rng = np.random.default_rng(0)
-    branch = [layers.ADMMDeconvF2((), K, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.02, 0.2, 2.0, 4.0)]
+    branch = [layers.ADMMDeconvF2((), K, r, layers.relu1, iso=args.iso, rng=rng, device=dev)
+              for r in (0.002, 0.02, 0.2, 2.0, 4.0)]
     for L in branch:
         L.lam.requires_grad_(True)
     nd = min(B, args.distinct)
@@ -133,7 +136,8 @@ def bench_c5(args, dev):
         "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
-                               "MSE, backward through admm_tvd_backward_f32 (aniso)", "global_batch": B},
+                               "MSE, backward through admm_tvd_backward_f32 "
+                               f"({'iso' if args.iso else 'aniso'})", "global_batch": B},
         "kernels": kernels}))
 
 
