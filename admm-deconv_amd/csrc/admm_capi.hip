@@ -104,8 +104,18 @@ int max_q(int NN) {
     }
     return NN;
 }
+// column block size: 1024 threads for long columns, so that a block covers >= 64 B of every row
+// (256 threads at N = 512 gave 4 slots = 32 B per row); ADMM_COL_THREADS overrides (256 or 1024)
+int column_threads(int N) {
+    int nt = N >= 512 ? 1024 : 256;
+    if (const char* e = getenv("ADMM_COL_THREADS")) {
+        const int v = atoi(e);
+        if (v == 256 || (v == 1024 && N >= 256)) nt = v;
+    }
+    return nt;
+}
 int column_KB(int M, int N) {
-    int KB = 256 / max_q(N);
+    int KB = column_threads(N) / max_q(N);
     if (KB > M / 2) KB = M / 2;
     if (KB > 32) KB = 32;
     return KB;
@@ -252,13 +262,22 @@ int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* s
 template <int MUL, bool SAVE, bool ACCQ>
 int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst, const float* C,
                     const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, float* Qp) {
+    const int nt = column_threads(N);
 #define X(v)                                                                                                   \
-    if (N == v) {                                                                                              \
+    if (N == v && nt == kThreads) {                                                                            \
         set_lds(column_kernel<v, MUL, SAVE, ACCQ>, lds);                                                       \
         column_kernel<v, MUL, SAVE, ACCQ><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \
         return 0;                                                                                              \
     }
     ADMM_N_CASES(X)
+#undef X
+#define X(v)                                                                                                   \
+    if (N == v && nt == 1024) {                                                                                \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 1024>, lds);                                                 \
+        column_kernel<v, MUL, SAVE, ACCQ, 1024><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \
+        return 0;                                                                                              \
+    }
+    X(256) X(512) X(1024)
 #undef X
     return -1;
 }

@@ -241,8 +241,8 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 //   SAVE   : also store the forward dim-2 spectrum (before the multiply) to vsave (trajectory for h_bar)
 //   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar)
 // ----------------------------------------------------------------------------------------------
-template <int NN, int MUL, bool SAVE, bool ACCQ>
-__global__ __launch_bounds__(kThreads) void column_kernel(const float2* src, float2* dst,
+template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
+__global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst,
                                                           const float* __restrict__ Ct,
                                                           const float2* __restrict__ Gt,
                                                           const float2* __restrict__ twN, int L, int KB, float cs,
