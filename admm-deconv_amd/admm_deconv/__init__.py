@@ -11,6 +11,7 @@ Package layout (the directory admm-deconv_amd/ is the product):
      parallel.py   batch sharding over ranks + RCCL gather
 """
 from ._lib import AdmmError, load, workspace_bytes  # noqa: F401
-from .ops import tvd_fft, tvd_fft_backward, Workspace  # noqa: F401
+from .ops import (tvd_fft, tvd_fft_backward, tvd_fft_record, tvd_fft_backward_recorded, Recording,  # noqa: F401
+                  Workspace)
 
 __version__ = "0.1.0"

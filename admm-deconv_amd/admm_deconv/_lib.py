@@ -26,6 +26,7 @@ KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: 
 EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "admm_tvd_forward_f32",
            "admm_tvd_backward_workspace_bytes", "admm_tvd_backward_f32",
            "admm_tvd_forward_sharded_f32", "admm_tvd_backward_sharded_f32",
+           "admm_tvd_forward_record_f32", "admm_tvd_backward_recorded_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
 
 
@@ -79,6 +80,12 @@ def load():
     L.admm_tvd_forward_sharded_f32.argtypes = list(L.admm_tvd_forward_f32.argtypes) + [ctypes.POINTER(BatchReducer)]
     L.admm_tvd_backward_sharded_f32.restype = c_int
     L.admm_tvd_backward_sharded_f32.argtypes = list(L.admm_tvd_backward_f32.argtypes) + [ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_forward_record_f32.restype = c_int
+    L.admm_tvd_forward_record_f32.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                              c_float, c_float, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p,
+                                              ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_backward_recorded_f32.restype = c_int
+    L.admm_tvd_backward_recorded_f32.argtypes = list(L.admm_tvd_backward_sharded_f32.argtypes)
     L.admm_profile_enable.restype = c_int
     L.admm_profile_enable.argtypes = [c_int]
     L.admm_profile_reset.restype = c_int

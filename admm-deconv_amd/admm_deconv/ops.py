@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["tvd_fft", "tvd_fft_backward", "Workspace"]
+__all__ = ["tvd_fft", "tvd_fft_backward", "tvd_fft_record", "tvd_fft_backward_recorded", "Recording", "Workspace"]
 
 
 class Workspace:
@@ -204,22 +204,92 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     return x.reshape(shape), y_bar.reshape(shape), h_bar, scal[0], scal[1]
 
 
+class Recording:
+    """One forward solve recorded for its adjoint (admm_tvd_forward_record_f32): the trajectory lives in
+    its own workspace until tvd_fft_backward_recorded consumes it, so a training step runs the forward
+    once (no recompute in the backward).  Memory: about 8 B/px per iteration (plus 8 B/px of dim-2
+    spectra per iteration with a PSF when h_bar is needed) -- sized for MI355X's 288 GB HBM."""
+
+    __slots__ = ("workspace", "y4", "hb", "shape", "lam", "rho", "iso", "maxit", "want_h", "group", "dims")
+
+
+def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, stream=None, group=None):
+    """Forward solve that records its trajectory.  Returns (x, Recording); see tvd_fft_backward_recorded."""
+    shape, y4, hb = _prep(y, h)
+    B, P, N, M = y4.shape
+    rec = Recording()
+    rec.lam, rec.rho = _scalar(lam, "lambda"), _scalar(rho, "rho")
+    kw, kh = (0, 0) if hb is None else hb.shape
+    rec.want_h = bool(need_h and hb is not None)
+    rec.y4, rec.hb, rec.shape, rec.iso, rec.maxit, rec.group = y4, hb, shape, bool(isotropic), int(maxit), group
+    rec.dims = (M, N, P, B, kh, kw)
+    nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, rec.want_h)
+    rec.workspace = Workspace()
+    ws_ptr, ws_len = rec.workspace.get(nbytes, y.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(y.device)
+    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    x = torch.empty_like(y4)
+    red, keep = _make_reducer(rec.workspace, group) if _sharded(isotropic, group) else (None, None)
+    _lib.check(_lib.load().admm_tvd_forward_record_f32(
+        y4.data_ptr(), x.data_ptr(), M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, rec.lam, rec.rho,
+        int(rec.iso), rec.maxit, int(rec.want_h), ws_ptr, ws_len, s_handle,
+        ctypes.byref(red) if red is not None else None))
+    del keep
+    return x.reshape(shape), rec
+
+
+def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None):
+    """Reverse sweep of a recorded forward (x = that forward's output, unmodified).  Returns
+    (y_bar, h_bar, lam_bar, rho_bar); h_bar is None unless the forward was recorded with need_h.
+    Consumes the recording (its workspace is released)."""
+    if rec.workspace is None:
+        raise RuntimeError("recording already consumed")
+    M, N, P, B, kh, kw = rec.dims
+    y4, hb = rec.y4, rec.hb
+    xb = x_bar.reshape(y4.shape).to(torch.float32).contiguous()
+    x4 = x.reshape(y4.shape)
+    if not x4.is_contiguous():
+        raise ValueError("x must be the recorded forward's (contiguous) output")
+    ws = rec.workspace
+    ws_ptr = ws._buf.data_ptr() + (-ws._buf.data_ptr()) % 256
+    ws_len = ws._buf.numel() - (-ws._buf.data_ptr()) % 256
+    if stream is None:
+        stream = torch.cuda.current_stream(y4.device)
+    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    y_bar = torch.empty_like(y4)
+    h_bar = torch.empty_like(hb) if rec.want_h else None
+    scal = torch.zeros(2, dtype=torch.float32, device=y4.device)
+    red, keep = _make_reducer(ws, rec.group) if _sharded(rec.iso, rec.group) else (None, None)
+    _lib.check(_lib.load().admm_tvd_backward_recorded_f32(
+        y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
+        scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, rec.lam, rec.rho,
+        int(rec.iso), rec.maxit, x4.data_ptr(), ws_ptr, ws_len, s_handle,
+        ctypes.byref(red) if red is not None else None))
+    del keep
+    rec.workspace = None    # released once the stream has consumed it (caching allocator is stream-ordered)
+    return y_bar.reshape(rec.shape), h_bar, scal[0], scal[1]
+
+
 class _TvdFFTFn(torch.autograd.Function):
     """Differentiable tvd_fft: forward through the HIP solve, backward through the HIP adjoint
     (the rrule the Julia shim would register, julia/ADMMDeconvHIP.jl)."""
 
     @staticmethod
     def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit, group):
-        ctx.save_for_backward(y, lam_t, rho_t, h_t)
-        ctx.iso, ctx.maxit, ctx.group = isotropic, maxit, group
-        return _forward_raw(y, lam_t, rho_t, h_t, isotropic, maxit, group=group)
+        # the forward records its trajectory; the backward runs only the reverse sweep from it
+        need_h = h_t.numel() > 0 and ctx.needs_input_grad[3]
+        x, ctx.rec = tvd_fft_record(y, lam_t, rho_t, h_t if h_t.numel() else None, isotropic, maxit,
+                                    need_h=need_h, group=group)
+        ctx.save_for_backward(lam_t, rho_t, h_t, x)   # x: version-checked (must stay unmodified)
+        return x
 
     @staticmethod
     def backward(ctx, x_bar):
-        y, lam_t, rho_t, h_t = ctx.saved_tensors
-        need_h = h_t is not None and h_t.numel() > 0 and ctx.needs_input_grad[3]
-        _, yb, hb, lb, rb = tvd_fft_backward(y, x_bar, lam_t, rho_t, h_t if h_t.numel() else None, ctx.iso,
-                                             ctx.maxit, need_h=need_h, group=ctx.group)
+        lam_t, rho_t, h_t, x = ctx.saved_tensors
+        need_h = ctx.rec.want_h
+        yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar)
+        ctx.rec = None
         hg = None
         if need_h:
             hg = hb.reshape(h_t.shape)

@@ -53,7 +53,28 @@ __device__ __forceinline__ void block_sum2(float a, float b, double* out, double
 //   vsum   : running sum of vbar (read-modify-write)   spec0 : rFFT_dim1 of g_{k-1}
 //   part   : per-block (rho_bar, tau_bar) partial sums
 // ----------------------------------------------------------------------------------------------
-template <int L, int T>
+// s of 4 pixels (i..i+3 of line j), both channels, from a plane's trajectory slot: the 2-pass layout
+// [ch][N][M], or (LN) the fused kernel's lane-native layout (plane_api.hpp: float4 (s0[p], s0[p+1],
+// s1[p], s1[p+1]) of pixel pair p = 4n + 2h of line j at [n][2j + h], M = 256)
+template <bool LN>
+__device__ __forceinline__ void load_s_quad(const float* __restrict__ sp, int j, int i, int M, size_t MN, bool c1_too,
+                                            float (&c0)[4], float (&c1)[4]) {
+    if constexpr (LN) {
+        const float4* q = reinterpret_cast<const float4*>(sp) + (size_t)(i >> 2) * 512 + 2 * j;
+        const float4 a = q[0], b = q[1];
+        c0[0] = a.x; c0[1] = a.y; c0[2] = b.x; c0[3] = b.y;
+        c1[0] = a.z; c1[1] = a.w; c1[2] = b.z; c1[3] = b.w;
+    } else {
+        const float4 a = *reinterpret_cast<const float4*>(sp + (size_t)j * M + i);
+        c0[0] = a.x; c0[1] = a.y; c0[2] = a.z; c0[3] = a.w;
+        if (c1_too) {
+            const float4 b = *reinterpret_cast<const float4*>(sp + MN + (size_t)j * M + i);
+            c1[0] = b.x; c1[1] = b.y; c1[2] = b.z; c1[3] = b.w;
+        }
+    }
+}
+
+template <int L, int T, bool LN = false>
 __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __restrict__ spec1,
                                                             const float* __restrict__ sk1, const float* __restrict__ sk,
                                                             const float* __restrict__ xK,
@@ -118,12 +139,8 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
         const bool own = t < T;
         float s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};   // s_{k-1}
         if (!first_k) {
-            const float4 a = *reinterpret_cast<const float4*>(sk1 + poff + off);
-            s0[0] = a.x; s0[1] = a.y; s0[2] = a.z; s0[3] = a.w;
-            if (own) {
-                const float4 b = *reinterpret_cast<const float4*>(sk1 + poff + MN + off);
-                s1[0] = b.x; s1[1] = b.y; s1[2] = b.z; s1[3] = b.w;
-            }
+            load_s_quad<LN>(sk1 + poff, (j0 + t) & (N - 1), i, M, MN, own, s0, s1);
+            if (!own) s1[0] = s1[1] = s1[2] = s1[3] = 0.0f;
         }
         if (own) {
             // ---- rho_bar: -<Dvb, D x_k> ----
@@ -136,9 +153,8 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
                 dx0[0] = xc.x - xq.x; dx0[1] = xc.y - xq.y; dx0[2] = xc.z - xq.z; dx0[3] = xc.w - xq.w;
                 dx1[0] = xc.x - xl; dx1[1] = xc.y - xc.x; dx1[2] = xc.z - xc.y; dx1[3] = xc.w - xc.z;
             } else {
-                const float4 a = *reinterpret_cast<const float4*>(sk + poff + off);
-                const float4 b = *reinterpret_cast<const float4*>(sk + poff + MN + off);
-                const float a4[4] = {a.x, a.y, a.z, a.w}, b4[4] = {b.x, b.y, b.z, b.w};
+                float a4[4], b4[4];
+                load_s_quad<LN>(sk + poff, (j0 + t) & (N - 1), i, M, MN, true, a4, b4);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     dx0[q] = a4[q] - fminf(fmaxf(s0[q], -tau), tau);

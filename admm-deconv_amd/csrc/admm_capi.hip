@@ -378,16 +378,16 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         return ADMM_OK;
     }
 
-    if (fused_shape(M, N, iso != 0) && !tr.s && !tr.v && fused_enabled()) {
+    if (fused_shape(M, N, iso != 0) && !tr.v && fused_enabled()) {
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
-        // spec0, lane-native s in sA
+        // spec0, lane-native s in sA -- or, recording a trajectory, s_k in its own slot of tr.s
         namespace pk = admm::plane;
         void* tables = ws + lay.F;
         rc = ln.run(ADMM_K_SETUP, [&] { (void)pk::launch_tables(Ct, Gt, tables, s); });
         if (rc) return rc;
         rc = ln.run(ADMM_K_PLANE, [&] {
             (void)pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), tau, rho, maxit,
-                                   planes, s);
+                                   planes, s, reinterpret_cast<float4*>(tr.s));
         });
         return rc;
     }
@@ -550,7 +550,19 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
 
 int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
                     const float* sk, const float* xK, const float* sb_in, float* sb_out, float* vsum, float2* spec0,
-                    double* part, const float2* twM, int N, float tau, float rho, int first_k, int last_k) {
+                    double* part, const float2* twM, int N, float tau, float rho, int first_k, int last_k, bool ln) {
+    if (ln) {   // trajectory in the fused kernel's lane-native layout (M = 256)
+#define X(l, t)                                                                                                \
+        if (L == l && T == t) {                                                                                \
+            set_lds(line_adj_kernel<l, t, true>, lds);                                                         \
+            line_adj_kernel<l, t, true><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, \
+                                                                  part, twM, N, tau, rho, first_k, last_k);    \
+            return 0;                                                                                          \
+        }
+        X(128, 2) X(128, 4) X(128, 8) X(128, 16)
+#undef X
+        return -1;
+    }
 #define X(l, t)                                                                                                \
     if (L == l && T == t) {                                                                                    \
         set_lds(line_adj_kernel<l, t>, lds);                                                                   \
@@ -645,20 +657,26 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
                                          rho, iso, maxit, x_out, workspace, workspace_bytes, stream, nullptr);
 }
 
-int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
-                                  float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
-                                  float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
-                                  size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+// phases: 1 = forward recording the trajectory into the workspace (writes x_out), 2 = reverse sweep
+// from a recorded workspace (x_out = that forward's output), 3 = both.  want_hbar_rec: phase 1 alone
+// records the extra h_bar trajectory only when asked (phase 2 must then be given h_bar).
+static int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                        float* lambda_bar, float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                        float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
+                        size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
     const admm_batch_reducer* red = (iso && reducer && reducer->fn) ? reducer : nullptr;
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    rc = check_common(y, y_bar, maxit, lambda, rho);
+    rc = check_common(y, (phases & 2) ? y_bar : x_out, maxit, lambda, rho);
     if (rc) return rc;
-    if (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)) return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
+    if ((phases & 2) && (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)))
+        return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
-    const bool want_h = h_bar != nullptr && kh > 0;
+    const bool want_h = (phases == 1 ? want_hbar_rec != 0 : h_bar != nullptr) && kh > 0;
+    // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
+    const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
     const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
@@ -681,11 +699,13 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
         if (e != hipSuccess) return fail(ADMM_E_HIP, "%s: %s", #call, hipGetErrorString(e));   \
     } while (0)
     if (K == 0) {
-        HIPCHK(hipMemsetAsync(y_bar, 0, planes * MN * 4, s));
-        if (h_bar && kh > 0) HIPCHK(hipMemsetAsync(h_bar, 0, (size_t)kh * kw * 4, s));
-        if (lambda_bar) HIPCHK(hipMemsetAsync(lambda_bar, 0, 4, s));
-        if (rho_bar) HIPCHK(hipMemsetAsync(rho_bar, 0, 4, s));
-        if (x_out) HIPCHK(hipMemsetAsync(x_out, 0, planes * MN * 4, s));
+        if (phases & 2) {
+            HIPCHK(hipMemsetAsync(y_bar, 0, planes * MN * 4, s));
+            if (h_bar && kh > 0) HIPCHK(hipMemsetAsync(h_bar, 0, (size_t)kh * kw * 4, s));
+            if (lambda_bar) HIPCHK(hipMemsetAsync(lambda_bar, 0, 4, s));
+            if (rho_bar) HIPCHK(hipMemsetAsync(rho_bar, 0, 4, s));
+        }
+        if (phases & 1) HIPCHK(hipMemsetAsync(x_out, 0, planes * MN * 4, s));
         return ln.finish();
     }
     // ---- forward with trajectory ----
@@ -694,8 +714,11 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
     tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
-    rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr, red);
-    if (rc) return rc;
+    if (phases & 1) {
+        rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr, red);
+        if (rc) return rc;
+    }
+    if (!(phases & 2)) return ln.finish();
     // ---- reverse sweep ----
     float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
     float2* twN = reinterpret_cast<float2*>(ws + bl.f.twN);
@@ -735,7 +758,7 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
         if (!iso) {
             rc = ln.run(ADMM_K_LINE, [&] {
                 launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
-                                k == 1 ? 1 : 0, k == K ? 1 : 0);
+                                k == 1 ? 1 : 0, k == K ? 1 : 0, ln_traj);
             });
             if (rc) return rc;
             continue;
@@ -819,6 +842,29 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
     if (rc) return rc;
 #undef HIPCHK
     return ln.finish();
+}
+
+int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                                  float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                                  float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
+                                  size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    return run_backward(3, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda, rho, iso,
+                        maxit, x_out, workspace, workspace_bytes, stream, reducer);
+}
+
+int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
+                                int kw, float lambda, float rho, int iso, int maxit, int want_hbar, void* workspace,
+                                size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    return run_backward(1, want_hbar, y, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, P, B, h, kh, kw, lambda,
+                        rho, iso, maxit, x_out, workspace, workspace_bytes, stream, reducer);
+}
+
+int admm_tvd_backward_recorded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                                   float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                                   float lambda, float rho, int iso, int maxit, const float* x_out, void* workspace,
+                                   size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    return run_backward(2, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda, rho, iso,
+                        maxit, const_cast<float*>(x_out), workspace, workspace_bytes, stream, reducer);
 }
 
 int admm_profile_enable(int on) {

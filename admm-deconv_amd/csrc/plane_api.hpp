@@ -23,8 +23,11 @@ inline size_t tables_bytes() { return (size_t)kTabEntries * 12 + 256 * 12 + 256;
 hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStream_t s);
 
 // all K >= 1 iterations for `planes` planes of 256 x 256; hln: planes x 256 KiB, sln: planes x 512 KiB
+// traj != NULL: record s_1..s_{K-1} for the adjoint, slot k-1 at traj + (k-1) * planes * 64 * 512
+// (lane-native: float4 (s0[p], s0[p+1], s1[p], s1[p+1]) of pixel pair p = 4n + 2h of line r at
+// [plane][n][2r + h]; s0 = x - x(line r-1), s1 = x - x(pixel p-1)); sln is then unused
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        float tau, float rho, int K, size_t planes, hipStream_t s);
+                        float tau, float rho, int K, size_t planes, hipStream_t s, float4* traj = nullptr);
 
 }  // namespace plane
 }  // namespace admm

@@ -269,7 +269,7 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 // 32..63 is parked in it (per-lane slots stg[m * 512 + t]) while registers 0..31 are processed; at
 // the half-way point the slots swap x[32+m] back in and v[m] out, and v[0..30] return at the end.
 // The chunk loop thus holds ~66 S registers instead of 128.
-__device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp, float2* xb,
+__device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sps, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho) {
     constexpr int CH = 2;            // registers per chunk
@@ -367,7 +367,7 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t hp
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
 #ifndef PLANE_EXPT_NOSTORE
-            bst4(sp, t * 16, n * kPT * 16, s);
+            bst4(sps, t * 16, n * kPT * 16, s);
 #endif
             wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
             hc[j + 1] = hyr[g % (PD + 1)][j];
@@ -429,12 +429,16 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
 }
 
 // grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
-template <bool PSF, int DBG = 0>
+// TRAJ: record the trajectory for the adjoint -- iteration k writes s_k to slot k-1 of `traj` (slot
+// stride traj_slot float4, lane-native layout, plane p at p * 64 * 512) and reads s_{k-1} from slot
+// k-2, instead of updating sln in place.  Same bytes per iteration as the plain solve.
+template <bool PSF, int DBG = 0, bool TRAJ = false>
 __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__ y, float* __restrict__ x_out,
                                                        const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
                                                        float2* __restrict__ hln, float4* __restrict__ sln, float tau,
-                                                       float rho, int K, float2* dbg = nullptr, int stagger_ticks = 0) {
+                                                       float rho, int K, float2* dbg = nullptr, int stagger_ticks = 0,
+                                                       float4* __restrict__ traj = nullptr, size_t traj_slot = 0) {
     // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
     // late, so that the memory-heavy row phases of two groups of CUs interleave.
     if (stagger_ticks > 0 && (blockIdx.x & 1)) {
@@ -485,7 +489,14 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         line_inverse_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
         if (k == K) break;
-        row_update(S, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+        if constexpr (TRAJ) {
+            float4* tb = traj + plane * 64 * kPT;
+            const rsrc_t sld = make_rsrc(tb + (size_t)(k >= 2 ? k - 2 : 0) * traj_slot, 64 * kPT * 16);
+            const rsrc_t sst = make_rsrc(tb + (size_t)(k - 1) * traj_slot, 64 * kPT * 16);
+            row_update(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+        } else {
+            row_update(S, sp, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+        }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
         line_forward_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k, t);

@@ -32,23 +32,29 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
     return hipGetLastError();
 }
 
+template <bool PSF, bool TRAJ>
+static void launch_one(const float* y, float* x_out, const Tables& t, float2* hln, float4* sln, float tau, float rho,
+                       int K, size_t planes, hipStream_t s, int stagger, float4* traj) {
+    (void)hipFuncSetAttribute((const void*)plane256_kernel<PSF, 0, TRAJ>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kLdsBytes);
+    hipLaunchKernelGGL((plane256_kernel<PSF, 0, TRAJ>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out,
+                       t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger, traj,
+                       planes * 64 * kPT);
+}
+
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        float tau, float rho, int K, size_t planes, hipStream_t s) {
+                        float tau, float rho, int K, size_t planes, hipStream_t s, float4* traj) {
     const Tables t = carve(tables);
     static const int stagger = [] {
         const char* e = getenv("ADMM_PLANE_STAGGER");   // experiment knob: realtime ticks (10 ns)
         return e ? atoi(e) : 0;
     }();
     if (psf) {
-        (void)hipFuncSetAttribute((const void*)plane256_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBytes);
-        hipLaunchKernelGGL(plane256_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf, t.C0b,
-                           t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger);
+        if (traj) launch_one<true, true>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
+        else launch_one<true, false>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
     } else {
-        (void)hipFuncSetAttribute((const void*)plane256_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBytes);
-        hipLaunchKernelGGL(plane256_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf,
-                           t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger);
+        if (traj) launch_one<false, true>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
+        else launch_one<false, false>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
     }
     return hipGetLastError();
 }

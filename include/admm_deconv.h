@@ -123,6 +123,24 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
                                   int maxit, float* x_out, void* workspace, size_t workspace_bytes,
                                   void* stream, const admm_batch_reducer* reducer);
 
+/* Split adjoint for a training step: the forward records its trajectory into `workspace` (sized by
+ * admm_tvd_backward_workspace_bytes with the same arguments and want_hbar), the backward later runs
+ * only the reverse sweep from it -- the forward is not recomputed.  Between the two calls the
+ * workspace must not be touched and x_out must still hold the recorded forward's output; y, h,
+ * lambda, rho, iso, maxit and the environment (ADMM_FUSED) must be the same.  h_bar must be
+ * non-NULL in the backward iff want_hbar was set in the forward.  With a reducer (iso, sharded
+ * batch) both calls must get one.  admm_tvd_backward_f32 is exactly the two calls back to back. */
+int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B,
+                                const float* h, int kh, int kw, float lambda, float rho, int iso,
+                                int maxit, int want_hbar, void* workspace, size_t workspace_bytes,
+                                void* stream, const admm_batch_reducer* reducer);
+int admm_tvd_backward_recorded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                                   float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
+                                   const float* h, int kh, int kw, float lambda, float rho, int iso,
+                                   int maxit, const float* x_out, void* workspace,
+                                   size_t workspace_bytes, void* stream,
+                                   const admm_batch_reducer* reducer);
+
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises
  * the stream before returning.  admm_profile_get returns the accumulated device time (ms) and

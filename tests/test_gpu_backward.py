@@ -142,3 +142,52 @@ def test_backward_deterministic(dev, iso):
     torch.cuda.synchronize()
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("with_psf", [False, True])
+def test_backward_fused_trajectory(dev, with_psf, monkeypatch):
+    """256 x 256 anisotropic without h_bar: the fused plane kernel records the trajectory (lane-native
+    s slots) and the reverse sweep reads it.  Against the fp64 oracle, and against the 2-pass
+    trajectory (ADMM_FUSED=0)."""
+    B, M, N, K, lam, rho = 2, 256, 256, 12, 0.0041, 0.021
+    h = synth.gaussian_psf(15, 2.5) if with_psf else None
+    y = synth.make_batch(B, M, N, h, g0=3)
+    xbar = np.random.default_rng(9).standard_normal(y.shape).astype(np.float32)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
+    x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(yt, xt, lam, rho, ht, False, K, need_h=False)
+    monkeypatch.setenv("ADMM_FUSED", "0")
+    x2, yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward(yt, xt, lam, rho, ht, False, K, need_h=False)
+    torch.cuda.synchronize()
+    assert hb is None
+    x0, yb0, _, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
+                                                      None if h is None else h.astype(np.float64), False, K, xbar)
+    assert_parity(x.cpu().numpy(), x0, what="x")
+    assert_grad(yb.cpu().numpy(), yb0, "y_bar")
+    assert_grad(yb.cpu().numpy(), yb2.cpu().numpy(), "y_bar fused vs 2-pass trajectory")
+    assert rel(float(lb), lb0) < 1e-2 and rel(float(rb), rb0) < 1e-2
+    assert rel(float(lb), float(lb2)) < 1e-2 and rel(float(rb), float(rb2)) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(2, 256, 256, None, False, False), (3, 64, 64, ("gauss", 7, 1.2), False, True),
+                                  (20, 32, 32, ("gauss", 5, 1.0), True, True), (2, 256, 256, ("gauss", 15, 2.5),
+                                                                                False, False)],
+                         ids=["256-fused", "64-psf-hbar", "32-iso", "256-psf-fused"])
+def test_record_then_backward_equals_combined(dev, case):
+    """admm_tvd_forward_record_f32 + admm_tvd_backward_recorded_f32 == admm_tvd_backward_f32, bitwise."""
+    B, M, N, spec, iso, need_h = case
+    h = psf(spec, None)
+    y = torch.from_numpy(synth.make_batch(B, M, N, h)).to(dev)
+    xb = torch.randn_like(y)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    K, lam, rho = 9, 0.01, 0.05
+    x, rec = admm_deconv.tvd_fft_record(y, lam, rho, ht, iso, K, need_h=need_h)
+    yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xb)
+    x2, yb2, hb2, lb2, rb2 = admm_deconv.tvd_fft_backward(y, xb, lam, rho, ht, iso, K, need_h=need_h)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x2) and torch.equal(yb, yb2)
+    assert torch.equal(lb, lb2) and torch.equal(rb, rb2)
+    if need_h:
+        assert torch.equal(hb, hb2)
+    with pytest.raises(RuntimeError):
+        admm_deconv.tvd_fft_backward_recorded(rec, x, xb)
