@@ -59,54 +59,53 @@ function tvd_fft(y::ROCArray{Float32, 4}, λ, ρ = Float32[1], h = ROCArray{Floa
 end
 
 # Zygote must not trace into the C call: the rule's pullback is the HIP adjoint through all `maxit`
-# unrolled iterations (admm_tvd_backward_f32, BASELINE config c5) -- what Zygote computes for the
-# reference by unrolling the loop (src/train.jl:51).  The backward recomputes the forward while
-# recording its trajectory, so the rule keeps no state between the two passes beyond its inputs.
-const _ws_bwd = Ref{Union{Nothing, ROCArray{UInt8, 1}}}(nothing)
-
-function _workspace_bwd(nbytes::Integer)
-    w = _ws_bwd[]
-    if w === nothing || length(w) < nbytes + 256
-        w = ROCArray{UInt8}(undef, nbytes + 256)
-        _ws_bwd[] = w
-    end
-    p = UInt(pointer(w))
-    off = (256 - p % 256) % 256
-    return Ptr{Cvoid}(p + off), Csize_t(length(w) - off)
-end
+# unrolled iterations -- what Zygote computes for the reference by unrolling the loop (src/train.jl:51).
+# The rule's forward records the trajectory (admm_tvd_forward_record_f32) into a workspace owned by
+# the pullback closure; the pullback runs only the reverse sweep (admm_tvd_backward_recorded_f32).
+# Memory per call: about 8 B/px per iteration (c5: ~4.8 GB per layer), sized for MI355X's 288 GB.
 
 # a tangent shaped like the 1-element λ / ρ the layer passes (Vector or ROCArray)
 _like(a::ROCArray, v) = ROCArray(fill(eltype(a)(v), size(a)))
 _like(a::AbstractArray, v) = fill(eltype(a)(v), size(a))
 _like(::Number, v) = v
 
+const _BwdSig = (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
+                 Cint, Cint, Cint, Cint, Ptr{Float32}, Cint, Cint, Cfloat, Cfloat, Cint, Cint,
+                 Ptr{Float32}, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cvoid})
+
 function ChainRulesCore.rrule(::typeof(tvd_fft), y::ROCArray{Float32, 4}, λ, ρ, h, isotropic, maxit)
-    x = tvd_fft(y, λ, ρ, h, isotropic, maxit)
+    M, N, P, B = size(y)
+    want_h = !isempty(h)
+    kh, kw = want_h ? (size(h, 1), size(h, 2)) : (0, 0)
+    hd = want_h ? (h isa ROCArray ? h : ROCArray(Float32.(h))) : nothing
+    lam, rho = Float32(Array(λ)[1]), Float32(Array(ρ)[1])
+    nbytes = Ref{Csize_t}(0)
+    rc = ccall((:admm_tvd_backward_workspace_bytes, LIB), Cint,
+               (Cint, Cint, Cint, Cint, Cint, Cint, Cint, Cint, Cint, Ref{Csize_t}),
+               M, N, P, B, kh, kw, isotropic, maxit, want_h, nbytes)
+    rc == 0 || error("admm_tvd_backward_workspace_bytes: ", _err())
+    rec = ROCArray{UInt8}(undef, nbytes[] + 256)          # the recording; lives in the closure
+    p = UInt(pointer(rec))
+    off = (256 - p % 256) % 256
+    ws, wslen = Ptr{Cvoid}(p + off), Csize_t(length(rec) - off)
+    x = similar(y)
+    rc = ccall((:admm_tvd_forward_record_f32, LIB), Cint,
+               (Ptr{Float32}, Ptr{Float32}, Cint, Cint, Cint, Cint, Ptr{Float32}, Cint, Cint, Cfloat, Cfloat,
+                Cint, Cint, Cint, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}, Ptr{Cvoid}),
+               pointer(y), pointer(x), M, N, P, B, want_h ? pointer(hd) : C_NULL, kh, kw, lam, rho,
+               isotropic, maxit, want_h, ws, wslen, AMDGPU.stream().stream, C_NULL)
+    rc == 0 || error("admm_tvd_forward_record_f32: ", _err())
     function tvd_fft_pullback(x̄)
         xb = ROCArray{Float32}(ChainRulesCore.unthunk(x̄))
-        M, N, P, B = size(y)
-        want_h = !isempty(h)
-        kh, kw = want_h ? (size(h, 1), size(h, 2)) : (0, 0)
-        hd = want_h ? (h isa ROCArray ? h : ROCArray(Float32.(h))) : nothing
-        nbytes = Ref{Csize_t}(0)
-        rc = ccall((:admm_tvd_backward_workspace_bytes, LIB), Cint,
-                   (Cint, Cint, Cint, Cint, Cint, Cint, Cint, Cint, Cint, Ref{Csize_t}),
-                   M, N, P, B, kh, kw, isotropic, maxit, want_h, nbytes)
-        rc == 0 || error("admm_tvd_backward_workspace_bytes: ", _err())
-        ws, wslen = _workspace_bwd(nbytes[])
         ȳ = similar(y)
-        xr = similar(y)
         h̄ = want_h ? similar(hd) : nothing
         scal = AMDGPU.zeros(Float32, 2)                  # (λ̄, ρ̄)
-        rc = ccall((:admm_tvd_backward_f32, LIB), Cint,
-                   (Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32}, Ptr{Float32},
-                    Cint, Cint, Cint, Cint, Ptr{Float32}, Cint, Cint, Cfloat, Cfloat, Cint, Cint,
-                    Ptr{Float32}, Ptr{Cvoid}, Csize_t, Ptr{Cvoid}),
+        rc = ccall((:admm_tvd_backward_recorded_f32, LIB), Cint, _BwdSig,
                    pointer(y), pointer(xb), pointer(ȳ), want_h ? pointer(h̄) : C_NULL, pointer(scal),
-                   pointer(scal) + 4, M, N, P, B, want_h ? pointer(hd) : C_NULL, kh, kw,
-                   Float32(Array(λ)[1]), Float32(Array(ρ)[1]), isotropic, maxit, pointer(xr), ws, wslen,
-                   AMDGPU.stream().stream)
-        rc == 0 || error("admm_tvd_backward_f32: ", _err())
+                   pointer(scal) + 4, M, N, P, B, want_h ? pointer(hd) : C_NULL, kh, kw, lam, rho,
+                   isotropic, maxit, pointer(x), ws, wslen, AMDGPU.stream().stream, C_NULL)
+        rc == 0 || error("admm_tvd_backward_recorded_f32: ", _err())
+        GC.@preserve rec nothing
         s = Array(scal)
         h̄t = want_h ? reshape(h̄, size(h)) : ChainRulesCore.NoTangent()
         return (ChainRulesCore.NoTangent(), ȳ, _like(λ, s[1]), _like(ρ, s[2]), h̄t,
