@@ -19,6 +19,7 @@
 
 #include "../../include/admm_deconv.h"
 #include "admm_kernels.hip"
+#include "admm_generic.hip"
 #include "admm_backward.hip"
 #include "plane_api.hpp"
 
@@ -40,8 +41,14 @@ int fail(int code, const char* fmt, ...) {
 bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 struct Layout {
-    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, total;
+    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, xg, total;
 };
+
+// The tuned kernels cover power-of-two 4 <= M <= 1024, 2 <= N <= 1024; every other shape from 2 x 2 up
+// to 4096 x 4096 runs the runtime-length path (admm_generic.hip).
+bool pow2_shape(int M, int N) { return is_pow2(M) && is_pow2(N) && M >= 4 && M <= 1024 && N >= 2 && N <= 1024; }
+bool generic_shape(int M, int N) { return !pow2_shape(M, N); }
+constexpr int kGenMax = 4096;
 
 // The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox;
 // ADMM_FUSED=0 forces the 2-pass path (tests compare the two).
@@ -72,8 +79,11 @@ Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.hty = psf ? take(planes * MN * 4) : 0;
     L.sA = take(planes * 2 * MN * 4);
     L.sB = take(planes * 2 * MN * 4);
-    L.spec0 = take(planes * MN * 4);  // N lines x M/2 complex
-    L.spec1 = take(planes * MN * 4);
+    // N lines x M/2 complex (packed) -- or M/2 + 1 bins per line on the generic path
+    const size_t spec_bytes = generic_shape(M, N) ? planes * (size_t)(M / 2 + 1) * N * 8 : planes * MN * 4;
+    L.spec0 = take(spec_bytes);
+    L.spec1 = take(spec_bytes);
+    L.xg = generic_shape(M, N) ? take(planes * MN * 4) : 0;
     L.fmap = iso ? take(MN * 4) : 0;
     L.part = iso ? take(((planes + kIsoGroup - 1) / kIsoGroup) * MN * 4) : 0;
     L.F = fused_shape(M, N, iso) ? take(fused_tables_bytes()) : 0;
@@ -300,8 +310,9 @@ int check_shape(int M, int N, int P, int B, int kh, int kw, int iso) {
     if (P < 1 || B < 1 || M < 1 || N < 1) return fail(ADMM_E_INVALID, "sizes must be positive (M=%d N=%d P=%d B=%d)", M, N, P, B);
     if (kh < 0 || kw < 0 || ((kh == 0) != (kw == 0)))
         return fail(ADMM_E_INVALID, "PSF size must be both zero (empty PSF) or both positive (kh=%d kw=%d)", kh, kw);
-    if (!is_pow2(M) || !is_pow2(N) || M < 4 || M > 1024 || N < 2 || N > 1024)
-        return fail(ADMM_E_UNSUPPORTED, "this build supports power-of-two 4<=M<=1024, 2<=N<=1024 (got M=%d N=%d)", M, N);
+    // M, N >= 2 as in the reference (ops.jl:32-33 index the second row / column of the D stencils)
+    if (M < 2 || N < 2 || M > kGenMax || N > kGenMax)
+        return fail(ADMM_E_UNSUPPORTED, "this build supports 2<=M<=%d, 2<=N<=%d (got M=%d N=%d)", kGenMax, kGenMax, M, N);
     if (kh > M || kw > N)
         return fail(ADMM_E_UNSUPPORTED, "PSF %dx%d larger than the image (kh<=M, kw<=N required, as pad_constant in ops.jl:25)", kh, kw);
     if (iso && (size_t)P * B > 65535)
@@ -339,6 +350,38 @@ struct Traj {
 
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
 // Returns the Launcher's status; `ln` keeps the events for the profiler.
+// ---- generic-size path (admm_generic.hip) ----------------------------------------------------
+admm::gen::FPlan make_fplan(int n) {
+    admm::gen::FPlan p{};
+    p.n = n;
+    int m = n;
+    auto add = [&](int r) { p.r[p.nf++] = r; m /= r; };
+    while (m % 8 == 0) add(8);
+    if (m % 4 == 0) add(4);
+    if (m % 2 == 0) add(2);
+    while (m % 3 == 0) add(3);
+    while (m % 5 == 0) add(5);
+    for (int f = 7; f * f <= m; f += 2)
+        while (m % f == 0) add(f);
+    if (m > 1) add(m);
+    return p;
+}
+// lines per block: the largest of 8, 4, 2, 1 dividing N with T * M <= 4096 (LDS ~ 24 T M bytes)
+int gen_T(int M, int N) {
+    for (int t = 8; t > 1; t >>= 1)
+        if (N % t == 0 && t * M <= 4096) return t;
+    return 1;
+}
+int gen_KB(int M, int N) {
+    int kb = 4096 / N;
+    kb = kb < 1 ? 1 : (kb > 16 ? 16 : kb);
+    return kb > M / 2 + 1 ? M / 2 + 1 : kb;
+}
+
+int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
+                        float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                        const admm_batch_reducer* red);
+
 // the caller's cross-shard sum of an M x N map (isotropic prox over a sharded batch)
 int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStream_t s) {
     const int r = red->fn(buf, count, reinterpret_cast<void*>(s), red->user);
@@ -368,6 +411,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         const size_t lds = (size_t)(M + N) * 16;
         const int nb = (int)(((size_t)(L + 1) * N + kThreads - 1) / kThreads);
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
+        set_lds(admm::setup_kernel, lds);
         hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Ct, Gt, h, kh, kw, M,
                            N, rho, SigT);
     });
@@ -378,6 +422,10 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         return ADMM_OK;
     }
 
+    if (generic_shape(M, N)) {
+        if (tr.s || tr.v) return fail(ADMM_E_UNSUPPORTED, "trajectory recording (adjoint) needs a power-of-two shape");
+        return run_forward_generic(ln, y, x_out, M, N, planes, kh, lambda, rho, iso, maxit, ws, lay, red);
+    }
     if (fused_shape(M, N, iso != 0) && !tr.v && fused_enabled()) {
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
         // spec0, lane-native s in sA -- or, recording a trajectory, s_k in its own slot of tr.s
@@ -473,6 +521,106 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         } else {
             rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
         }
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
+int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
+                        float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                        const admm_batch_reducer* red) {
+    namespace g = admm::gen;
+    hipStream_t s = ln.s;
+    int rc = ADMM_OK;
+    const size_t MN = (size_t)M * N;
+    const int H = M / 2 + 1;
+    const float2* twM = reinterpret_cast<float2*>(ws + lay.twM);
+    const float2* twN = reinterpret_cast<float2*>(ws + lay.twN);
+    const float* Ct = reinterpret_cast<float*>(ws + lay.C);
+    const float2* Gt = kh > 0 ? reinterpret_cast<float2*>(ws + lay.G) : nullptr;
+    const float* hty = kh > 0 ? reinterpret_cast<float*>(ws + lay.hty) : y;
+    float* sbuf[2] = {reinterpret_cast<float*>(ws + lay.sA), reinterpret_cast<float*>(ws + lay.sB)};
+    float2* spec0 = reinterpret_cast<float2*>(ws + lay.spec0);
+    float2* spec1 = reinterpret_cast<float2*>(ws + lay.spec1);
+    float* xg = reinterpret_cast<float*>(ws + lay.xg);
+    float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
+    float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
+    const float tau = lambda / rho;
+    const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
+    const int T = gen_T(M, N), KB = gen_KB(M, N);
+    const dim3 gl(N / T, (unsigned)planes), gc((H + KB - 1) / KB, (unsigned)planes);
+    const size_t lfw = (size_t)2 * T * M * 8;                        // line_fwd / line_inv
+    const size_t lup = lfw + (size_t)(2 * T + 1) * M * 4;            // line_upd / iso_b
+    const size_t lcol = (size_t)2 * KB * N * 8;
+    set_lds(g::line_fwd_kernel, lfw);
+    set_lds(g::line_inv_kernel, lfw);
+    set_lds(g::line_upd_kernel, lup);
+    set_lds(g::iso_b_kernel, lup);
+    set_lds(g::column_kernel, lcol);
+    // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
+    rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, y, spec0, twM, pM, N, T); });
+    if (rc) return rc;
+    if (kh > 0) {
+        rc = ln.run(ADMM_K_PREP, [&] {
+            hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 1, 1.0f);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_PREP, [&] {
+            hipLaunchKernelGGL(g::line_inv_kernel, gl, dim3(256), lfw, s, spec1, const_cast<float*>(hty), twM, pM, N, T);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, hty, spec0, twM, pM, N, T); });
+        if (rc) return rc;
+    }
+    const int ng = (int)((planes + kIsoGroup - 1) / kIsoGroup);
+    for (int it = 1; it <= maxit; ++it) {
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 0, 1.0f);
+        });
+        if (rc) return rc;
+        const bool last = it == maxit;
+        rc = ln.run(last ? ADMM_K_FINAL : ADMM_K_LINE, [&] {
+            hipLaunchKernelGGL(g::line_inv_kernel, gl, dim3(256), lfw, s, spec1, last ? x_out : xg, twM, pM, N, T);
+        });
+        if (rc) return rc;
+        if (last) break;
+        if (!iso) {
+            float* so = (it & 1) ? sbuf[1] : sbuf[0];   // iteration 1 reads nothing (first)
+            float* sn = (it & 1) ? sbuf[0] : sbuf[1];
+            rc = ln.run(ADMM_K_LINE, [&] {
+                hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, tau,
+                                   rho, it == 1 ? 1 : 0);
+            });
+            if (rc) return rc;
+            continue;
+        }
+        float* sa = sbuf[0];
+        rc = ln.run(ADMM_K_LINE, [&] {
+            hipLaunchKernelGGL(g::iso_a_kernel, dim3(N / T, ng), dim3(256), (size_t)T * M * 4, s, xg, sa, fmap, part, M,
+                               N, (int)planes, kIsoGroup, T, it == 1 ? 1 : 0);
+        });
+        if (rc) return rc;
+        const int nb = (int)((MN + kThreads - 1) / kThreads);
+        const dim3 gr(nb < 2048 ? nb : 2048);
+        if (red) {
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_sum_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN);
+            });
+            if (rc) return rc;
+            rc = call_reducer(red, fmap, MN, s);
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, (float*)nullptr);
+            });
+        } else {
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, (float*)nullptr);
+            });
+        }
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_LINE, [&] {
+            hipLaunchKernelGGL(g::iso_b_kernel, gl, dim3(256), lup, s, sa, fmap, hty, spec0, twM, pM, N, T, rho);
+        });
         if (rc) return rc;
     }
     return ADMM_OK;
@@ -645,6 +793,9 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
+    if (generic_shape(M, N))
+        return fail(ADMM_E_UNSUPPORTED, "the adjoint needs a power-of-two shape (4<=M<=1024, 2<=N<=1024; got M=%d N=%d)",
+                    M, N);
     *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
     return ADMM_OK;
 }
@@ -674,6 +825,9 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
+    if (generic_shape(M, N))
+        return fail(ADMM_E_UNSUPPORTED, "the adjoint needs a power-of-two shape (4<=M<=1024, 2<=N<=1024; got M=%d N=%d)",
+                    M, N);
     const bool want_h = (phases == 1 ? want_hbar_rec != 0 : h_bar != nullptr) && kh > 0;
     // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
     const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;

@@ -1,0 +1,332 @@
+// admm_generic.hip -- the solve for shapes outside the power-of-two kernels' support matrix.
+//
+// The reference accepts any M x N (FFTW / CUFFT plans, /root/reference/src/ops/ops.jl:26,35-36,86 and
+// :108,117-118,168), e.g. 96 x 96 demos or 480 x 640 photographs.  The tuned path (admm_kernels.hip,
+// plane_kernel.hip) is specialised for powers of two; this file keeps the same 2-pass structure with
+// RUNTIME lengths:
+//   * mixed-radix Stockham FFTs staged in LDS, radix 8/4/2/3/5 butterflies in registers and a direct
+//     DFT for any other prime factor (so every length works; 2-3-5-smooth lengths are the fast case);
+//   * dim-1 (contiguous, real) transforms as full complex FFTs of the real line, keeping bins
+//     0..M/2 (the rfft half spectrum, ops.jl:86) -- M may be odd;
+//   * per iteration: GEN_COLUMN (dim-2 FFT, x C/(MN), inverse) -> GEN_LINE_INV (x to HBM) ->
+//     GEN_LINE_UPD (D, prox, dual, D^T, + H^T y, dim-1 FFT) -- or the iso triple GEN_ISO_A -> ISO_R ->
+//     GEN_ISO_B.  x takes one extra HBM round trip compared with the fused line kernel (8 B/px).
+// Spectrum layout: [plane][line j][bin k], H = M/2 + 1 bins per line (k fastest).
+#include <hip/hip_runtime.h>
+
+namespace admm {
+namespace gen {
+
+constexpr int kMaxF = 24;
+// factorisation of a transform length, applied in this order (built on the host)
+struct FPlan {
+    int n, nf;
+    int r[kMaxF];
+};
+
+template <bool INV>
+__device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int t) {
+    const float2 w = tw[t];   // exp(-2 pi i t / n)
+    return INV ? cconj(w) : w;
+}
+__device__ __forceinline__ float2 mul_i(float2 z) { return make_float2(-z.y, z.x); }
+
+template <bool INV>
+__device__ __forceinline__ void dft3(float2& a, float2& b, float2& c) {
+    constexpr float c1 = -0.5f;
+    constexpr float s1 = INV ? 0.866025403784438647f : -0.866025403784438647f;
+    const float2 t = cadd(b, c), d = cscale(csub(b, c), s1);
+    const float2 m = make_float2(fmaf(c1, t.x, a.x), fmaf(c1, t.y, a.y));
+    a = cadd(a, t);
+    b = cadd(m, mul_i(d));
+    c = csub(m, mul_i(d));
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft5(float2 (&x)[5]) {
+    constexpr float c1 = 0.309016994374947424f, c2 = -0.809016994374947424f;
+    constexpr float sg = INV ? 1.0f : -1.0f;
+    constexpr float s1 = sg * 0.951056516295153572f, s2 = sg * 0.587785252292473129f;
+    const float2 t1 = cadd(x[1], x[4]), t2 = cadd(x[2], x[3]);
+    const float2 d1 = csub(x[1], x[4]), d2 = csub(x[2], x[3]);
+    const float2 m1 = make_float2(x[0].x + c1 * t1.x + c2 * t2.x, x[0].y + c1 * t1.y + c2 * t2.y);
+    const float2 m2 = make_float2(x[0].x + c2 * t1.x + c1 * t2.x, x[0].y + c2 * t1.y + c1 * t2.y);
+    const float2 e1 = mul_i(make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y));
+    const float2 e2 = mul_i(make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y));
+    x[0] = cadd(x[0], cadd(t1, t2));
+    x[1] = cadd(m1, e1);
+    x[4] = csub(m1, e1);
+    x[2] = cadd(m2, e2);
+    x[3] = csub(m2, e2);
+}
+
+// one radix-R butterfly of a Stockham pass: src[j + a q] (a < R) twiddled by W_{Ns R}^{a k}, DFT_R,
+// to dst[(j / Ns) Ns R + k + c Ns]
+template <int R, bool INV>
+__device__ __forceinline__ void bfly(const float2* __restrict__ src, float2* __restrict__ dst, int j, int q, int Ns,
+                                     int tstep, const float2* __restrict__ tw) {
+    const int k = j % Ns;
+    float2 v[R];
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+        v[a] = src[j + a * q];
+        if (a > 0 && k > 0) v[a] = cmul(v[a], twid<INV>(tw, a * k * tstep));
+    }
+    if constexpr (R == 3) {
+        dft3<INV>(v[0], v[1], v[2]);
+    } else if constexpr (R == 5) {
+        dft5<INV>(v);
+    } else {
+        dft<R, INV>(v);
+    }
+    const int base = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int c = 0; c < R; ++c) dst[base + c * Ns] = v[c];
+}
+
+// any radix (prime factors other than 2, 3, 5): direct O(R^2) evaluation from LDS
+template <bool INV>
+__device__ __forceinline__ void bfly_any(const float2* __restrict__ src, float2* __restrict__ dst, int j, int q,
+                                         int Ns, int R, int n, int tstep, const float2* __restrict__ tw) {
+    const int k = j % Ns;
+    const int base = (j / Ns) * Ns * R + k;
+    const int rstep = n / R;
+    for (int c = 0; c < R; ++c) {
+        float2 acc = make_float2(0.f, 0.f);
+        for (int a = 0; a < R; ++a) {
+            float2 x = src[j + a * q];
+            if (a > 0 && k > 0) x = cmul(x, twid<INV>(tw, a * k * tstep));
+            acc = cadd(acc, cmul(x, twid<INV>(tw, ((a * c) % R) * rstep)));
+        }
+        dst[base + c * Ns] = acc;
+    }
+}
+
+// cnt transforms of length pl.n at a[t * stride ...]; ping-pong with b; returns the buffer holding the
+// result.  The caller synchronises before (input ready) -- every pass ends with a block barrier.
+template <bool INV>
+__device__ float2* fft(float2* a, float2* b, int cnt, int stride, const FPlan& pl, const float2* __restrict__ tw) {
+    int Ns = 1;
+    const int n = pl.n;
+    for (int p = 0; p < pl.nf; ++p) {
+        const int R = pl.r[p];
+        const int q = n / R;
+        const int tstep = n / (Ns * R);
+        for (int idx = threadIdx.x; idx < cnt * q; idx += blockDim.x) {
+            const int line = idx / q, j = idx - line * q;
+            const float2* src = a + (size_t)line * stride;
+            float2* dst = b + (size_t)line * stride;
+            switch (R) {
+                case 2: bfly<2, INV>(src, dst, j, q, Ns, tstep, tw); break;
+                case 3: bfly<3, INV>(src, dst, j, q, Ns, tstep, tw); break;
+                case 4: bfly<4, INV>(src, dst, j, q, Ns, tstep, tw); break;
+                case 5: bfly<5, INV>(src, dst, j, q, Ns, tstep, tw); break;
+                case 8: bfly<8, INV>(src, dst, j, q, Ns, tstep, tw); break;
+                default: bfly_any<INV>(src, dst, j, q, Ns, R, n, tstep, tw); break;
+            }
+        }
+        __syncthreads();
+        Ns *= R;
+        float2* t = a;
+        a = b;
+        b = t;
+    }
+    return a;
+}
+
+__device__ __forceinline__ int wrap(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+__device__ __forceinline__ float clip(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
+__device__ __forceinline__ float phi(float s, float tau) { return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s; }
+
+// real lines -> half spectra (T lines per block, grid (N / T, planes))
+__global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__ src, float2* __restrict__ spec,
+                                                       const float2* __restrict__ twM, FPlan pM, int N, int T) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int M = pM.n, H = M / 2 + 1;
+    float2* A = reinterpret_cast<float2*>(smem_raw);
+    float2* B = A + (size_t)T * M;
+    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const float* sp = src + ((size_t)plane * N + j0) * M;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) A[idx] = make_float2(sp[idx], 0.0f);
+    __syncthreads();
+    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    float2* dp = spec + ((size_t)plane * N + j0) * H;
+    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
+        const int t = idx / H, k = idx - t * H;
+        dp[idx] = R[t * M + k];
+    }
+}
+
+// half spectra -> real lines (Hermitian extension, complex inverse, real part; unnormalised)
+__global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict__ spec, float* __restrict__ dst,
+                                                       const float2* __restrict__ twM, FPlan pM, int N, int T) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int M = pM.n, H = M / 2 + 1;
+    float2* A = reinterpret_cast<float2*>(smem_raw);
+    float2* B = A + (size_t)T * M;
+    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const float2* sp = spec + ((size_t)plane * N + j0) * H;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        const int t = idx / M, k = idx - t * M;
+        A[idx] = k < H ? sp[t * H + k] : cconj(sp[t * H + (M - k)]);
+    }
+    __syncthreads();
+    const float2* R = fft<true>(A, B, T, M, pM, twM);
+    float* dp = dst + ((size_t)plane * N + j0) * M;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) dp[idx] = R[idx].x;
+}
+
+// dim-2 transforms of KB spectral columns: FFT_N, x multiplier, IFFT_N (grid (ceil(H / KB), planes)).
+//   mode 0: x cs * Ct (x-update C / (MN), ops.jl:86);  mode 1: x Gt (H^T: conj(Sigma_c) / (MN))
+__global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
+                                                     const float* __restrict__ Ct, const float2* __restrict__ Gt,
+                                                     const float2* __restrict__ twN, FPlan pN, int H, int KB,
+                                                     int mode, float cs) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int N = pN.n;
+    float2* A = reinterpret_cast<float2*>(smem_raw);
+    float2* B = A + (size_t)KB * N;
+    const int plane = blockIdx.y, k0 = blockIdx.x * KB;
+    const int kc = min(KB, H - k0);
+    const float2* sp = src + (size_t)plane * N * H + k0;
+    float2* dp = dst + (size_t)plane * N * H + k0;
+    for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
+        const int j = idx / KB, c = idx - j * KB;
+        A[c * N + j] = c < kc ? sp[(size_t)j * H + c] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    float2* R = fft<false>(A, B, KB, N, pN, twN);
+    float2* O = R == A ? B : A;
+    for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
+        const int kj = idx / KB, c = idx - kj * KB;
+        if (c >= kc) continue;
+        const size_t q = (size_t)kj * H + k0 + c;
+        const float2 v = R[c * N + kj];
+        R[c * N + kj] = mode == 0 ? cscale(v, cs * Ct[q]) : cmul(v, Gt[q]);
+    }
+    __syncthreads();
+    const float2* Z = fft<true>(R, O, KB, N, pN, twN);
+    for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
+        const int j = idx / KB, c = idx - j * KB;
+        if (c < kc) dp[(size_t)j * H + c] = Z[c * N + j];
+    }
+}
+
+// line update (aniso, iterations 1..K-1) for T lines: s = D x + clip(s_old), w = phi(s),
+// v = H^T y + rho D^T w -> half spectrum.  s_old / s_new must not alias (halo line of s_old).
+__global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__ x, const float* __restrict__ s_old,
+                                                       float* __restrict__ s_new, const float* __restrict__ hty,
+                                                       float2* __restrict__ spec, const float2* __restrict__ twM,
+                                                       FPlan pM, int N, int T, float tau, float rho, int first) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int M = pM.n, H = M / 2 + 1;
+    const size_t MN = (size_t)M * N;
+    float2* A = reinterpret_cast<float2*>(smem_raw);
+    float2* B = A + (size_t)T * M;
+    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);   // T+1 lines
+    float* W1 = W0 + (size_t)(T + 1) * M;                       // T lines
+    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const float* xp = x + (size_t)plane * MN;
+    const float* so = s_old + (size_t)plane * 2 * MN;
+    float* sn = s_new + (size_t)plane * 2 * MN;
+    for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
+        const int t = idx / M, i = idx - t * M;
+        const int jj = wrap(j0 + t, N), jp = wrap(jj - 1, N);
+        const size_t o = (size_t)jj * M + i;
+        const float xc = xp[o];
+        const float s0 = xc - xp[(size_t)jp * M + i] + (first ? 0.0f : clip(so[o], tau));
+        W0[idx] = phi(s0, tau);
+        if (t < T) {
+            const float s1 = xc - xp[(size_t)jj * M + wrap(i - 1, M)] + (first ? 0.0f : clip(so[MN + o], tau));
+            W1[idx] = phi(s1, tau);
+            sn[o] = s0;
+            sn[MN + o] = s1;
+        }
+    }
+    __syncthreads();
+    const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        const int t = idx / M, i = idx - t * M;
+        const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
+        A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
+    }
+    __syncthreads();
+    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    float2* dp = spec + ((size_t)plane * N + j0) * H;
+    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
+        const int t = idx / H, k = idx - t * H;
+        dp[idx] = R[t * M + k];
+    }
+}
+
+// isotropic step A (grid (N / T, plane groups)): s = D x + (1 - f_old) s_old written in place, and the
+// group's partial sum of s^2 over planes and both channels per pixel (ops.jl:6)
+__global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x, float* s, const float* __restrict__ fmap,
+                                                    float* __restrict__ part, int M, int N, int planes, int G, int T,
+                                                    int first) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float* acc = reinterpret_cast<float*>(smem_raw);
+    const size_t MN = (size_t)M * N;
+    const int j0 = blockIdx.x * T, grp = blockIdx.y;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) acc[idx] = 0.0f;
+    const int p_end = min(planes, (grp + 1) * G);
+    for (int plane = grp * G; plane < p_end; ++plane) {
+        const float* xp = x + (size_t)plane * MN;
+        float* sp = s + (size_t)plane * 2 * MN;
+        for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+            const int t = idx / M, i = idx - t * M;
+            const int jj = j0 + t, jp = wrap(jj - 1, N);
+            const size_t o = (size_t)jj * M + i;
+            const float f = first ? 0.0f : fmap[o];
+            const float xc = xp[o];
+            const float a0 = first ? 0.0f : sp[o], a1 = first ? 0.0f : sp[MN + o];
+            const float s0 = (xc - xp[(size_t)jp * M + i]) + (a0 - f * a0);
+            const float s1 = (xc - xp[(size_t)jj * M + wrap(i - 1, M)]) + (a1 - f * a1);
+            sp[o] = s0;
+            sp[MN + o] = s1;
+            acc[idx] += s0 * s0 + s1 * s1;   // each idx is owned by one thread
+        }
+    }
+    float* pp = part + (size_t)grp * MN + (size_t)j0 * M;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) pp[idx] = acc[idx];
+}
+
+// isotropic step B: w = (2f - 1) s, v = H^T y + rho D^T w -> half spectrum
+__global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s, const float* __restrict__ fmap,
+                                                    const float* __restrict__ hty, float2* __restrict__ spec,
+                                                    const float2* __restrict__ twM, FPlan pM, int N, int T,
+                                                    float rho) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int M = pM.n, H = M / 2 + 1;
+    const size_t MN = (size_t)M * N;
+    float2* A = reinterpret_cast<float2*>(smem_raw);
+    float2* B = A + (size_t)T * M;
+    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);
+    float* W1 = W0 + (size_t)(T + 1) * M;
+    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const float* sp = s + (size_t)plane * 2 * MN;
+    for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
+        const int t = idx / M, i = idx - t * M;
+        const size_t o = (size_t)wrap(j0 + t, N) * M + i;
+        const float f = fmap[o];
+        W0[idx] = f * sp[o] - (sp[o] - f * sp[o]);
+        if (t < T) W1[idx] = f * sp[MN + o] - (sp[MN + o] - f * sp[MN + o]);
+    }
+    __syncthreads();
+    const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        const int t = idx / M, i = idx - t * M;
+        const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
+        A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
+    }
+    __syncthreads();
+    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    float2* dp = spec + ((size_t)plane * N + j0) * H;
+    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
+        const int t = idx / H, k = idx - t * H;
+        dp[idx] = R[t * M + k];
+    }
+}
+
+}  // namespace gen
+}  // namespace admm

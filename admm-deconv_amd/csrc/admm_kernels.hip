@@ -92,11 +92,11 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
         if (kh > 0) {
             double re = 0.0, im = 0.0;
             for (int b = 0; b < kw; ++b) {
-                const double2 eb = tN[(b * kj) & (N - 1)];
+                const double2 eb = tN[(b * kj) % N];
                 double gr = 0.0, gi = 0.0;
                 for (int a = 0; a < kh; ++a) {
                     const double w = (double)h[b * kh + a];
-                    const double2 ea = tM[(a * k) & (M - 1)];
+                    const double2 ea = tM[(a * k) % M];
                     gr += w * ea.x;
                     gi += w * ea.y;
                 }
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
             s2 = re * re + im * im;
             if (SigT) SigT[q] = make_double2(re, im);   // top-left PSF spectrum (backward h_bar)
             // centred spectrum: Sigma_c = Sigma * exp(+2 pi i (padd k/M + padr kj/N)); store conj / (MN)
-            const double2 pa = tM[(padd * k) & (M - 1)];
-            const double2 pb = tN[(padr * kj) & (N - 1)];
+            const double2 pa = tM[(padd * k) % M];
+            const double2 pb = tN[(padr * kj) % N];
             const double pr = pa.x * pb.x - pa.y * pb.y, pi = pa.x * pb.y + pa.y * pb.x;  // exp(-i phi)
             // Sigma_c = Sigma * conj(p);  conj(Sigma_c) = conj(Sigma) * p
             const double cr = re * pr + im * pi;

@@ -20,9 +20,10 @@
  *    `y` is never modified; the result goes to `x_out` (the reference returns a new array).
  *  - Return value: 0 on success, a negative ADMM_E* code otherwise; admm_last_error() gives a
  *    thread-local message for the last failing call.
- *  - Supported shapes (this build): M, N powers of two with 4 <= M <= 1024, 2 <= N <= 1024;
- *    kh <= M, kw <= N.  Other shapes return ADMM_E_UNSUPPORTED (the reference accepts any
- *    M x N through FFTW/CUFFT; non-power-of-two sizes are a listed next step).
+ *  - Supported shapes: any 2 <= M, N <= 4096 with kh <= M, kw <= N (the reference accepts any
+ *    M x N >= 2 x 2 through FFTW/CUFFT).  Powers of two with 4 <= M <= 1024, 2 <= N <= 1024 run
+ *    the tuned kernels; every other shape runs a runtime-length mixed-radix path (forward only:
+ *    the adjoint returns ADMM_E_UNSUPPORTED for those shapes). 
  */
 #ifndef ADMM_DECONV_H
 #define ADMM_DECONV_H

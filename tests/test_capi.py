@@ -36,8 +36,10 @@ def test_workspace_bytes():
 
 
 @pytest.mark.parametrize("args,code", [
-    ((48, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),   # non-power-of-two M
-    ((64, 2048, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large
+    ((8192, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # M too large
+    ((64, 8192, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large
+    ((1, 64, 1, 1, 0, 0, 0), _lib.ADMM_E_UNSUPPORTED),     # M < 2 (ops.jl:33 needs a second row)
+    ((64, 1, 1, 1, 0, 0, 0), _lib.ADMM_E_UNSUPPORTED),     # N < 2
     ((64, 64, 1, 1, 5, 0, 0), _lib.ADMM_E_INVALID),        # half-empty PSF
     ((64, 64, 0, 1, 5, 5, 0), _lib.ADMM_E_INVALID),        # P = 0
     ((64, 64, 1, 1, 65, 5, 0), _lib.ADMM_E_UNSUPPORTED),   # PSF taller than the image
@@ -69,3 +71,13 @@ def test_product_path_has_no_cpu_fallback():
     from admm_deconv import tvd_fft
     with pytest.raises(TypeError):
         tvd_fft(torch.zeros(1, 1, 8, 8), 0.1, 1.0)
+
+
+@pytest.mark.parametrize("M,N", [(48, 64), (100, 75), (37, 29), (64, 2048)])
+def test_generic_shapes_forward_only(M, N):
+    """Shapes outside the power-of-two kernels run the generic path (forward); the adjoint refuses them."""
+    out = ctypes.c_size_t(0)
+    L = _lib.load()
+    assert L.admm_tvd_workspace_bytes(M, N, 1, 2, 5, 5, 0, ctypes.byref(out)) == _lib.ADMM_OK
+    assert out.value >= 2 * M * N * 4 * 4
+    assert L.admm_tvd_backward_workspace_bytes(M, N, 1, 2, 5, 5, 0, 4, 0, ctypes.byref(out)) == _lib.ADMM_E_UNSUPPORTED

@@ -67,6 +67,34 @@ def test_parity_vs_oracle(dev, case):
     assert_parity(got, ref, what=str(case))
 
 
+# shapes outside the power-of-two kernels: the runtime-length path (admm_generic.hip), any M, N
+GENERIC_CASES = [
+    # (B, P, N, M, psf, lam, rho, K, iso)
+    (2, 1, 48, 48, ("gauss", 9, 1.2), 0.0041, 0.021, 10, False),    # 2^4 * 3
+    (1, 2, 96, 80, ("rand", 7, 4), 0.01, 0.05, 8, False),           # 2-3-5 smooth, asymmetric PSF
+    (1, 1, 45, 63, ("rand", 10, 10), 0.02, 0.1, 6, False),          # odd M and N, even PSF
+    (1, 1, 37, 29, ("gauss", 5, 1.0), 0.02, 0.1, 5, False),         # primes (direct-DFT radix)
+    (2, 1, 100, 75, None, 0.05, 0.02, 12, False),                   # empty PSF
+    (1, 1, 2048, 64, ("gauss", 5, 1.0), 0.0041, 0.021, 3, False),   # power of two beyond the tuned range
+    (1, 1, 30, 2, None, 0.05, 0.3, 4, False),                       # M = 2
+    (1, 1, 480, 640, ("gauss", 15, 2.5), 0.0041, 0.021, 5, False),  # a photograph
+    (20, 1, 40, 24, ("gauss", 5, 1.0), 0.02, 0.1, 6, True),         # isotropic, two plane groups
+    (2, 3, 33, 50, None, 0.05, 0.1, 7, True),
+]
+
+
+@pytest.mark.parametrize("case", GENERIC_CASES,
+                         ids=[f"{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}{'-iso' if c[8] else ''}" for c in GENERIC_CASES])
+def test_generic_shape_parity_vs_oracle(dev, case):
+    B, P, N, M, psf, lam, rho, K, iso = case
+    rng = np.random.default_rng(B * 7 + N + 3 * M + K)
+    h = make_psf(psf, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=2)
+    got = run_gpu(dev, y, lam, rho, h, iso, K)
+    ref = run_oracle(y, lam, rho, h, iso, K)
+    assert_parity(got, ref, what=str(case))
+
+
 def test_maxit_zero_returns_zeros(dev):
     y = np.random.default_rng(0).random((2, 1, 16, 16)).astype(np.float32)
     got = run_gpu(dev, y, 0.01, 0.1, None, False, 0)
