@@ -27,6 +27,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_tvd_backward_workspace_bytes", "admm_tvd_backward_f32",
            "admm_tvd_forward_sharded_f32", "admm_tvd_backward_sharded_f32",
            "admm_tvd_forward_record_f32", "admm_tvd_backward_recorded_f32",
+           "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
 
 
@@ -86,6 +87,17 @@ def load():
                                               ctypes.POINTER(BatchReducer)]
     L.admm_tvd_backward_recorded_f32.restype = c_int
     L.admm_tvd_backward_recorded_f32.argtypes = list(L.admm_tvd_backward_sharded_f32.argtypes)
+    L.admm_metrics_workspace_bytes.restype = c_int
+    L.admm_metrics_workspace_bytes.argtypes = [c_int] * 6 + [ctypes.POINTER(c_size_t)]
+    L.admm_gmsd_f32.restype = c_int
+    L.admm_gmsd_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [c_float, c_float, c_void_p, c_void_p, c_void_p,
+                                                                     c_void_p, c_size_t, c_void_p]
+    L.admm_ssim_f32.restype = c_int
+    L.admm_ssim_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [ctypes.POINTER(c_float), c_int, c_float, c_int,
+                                                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                                                     c_void_p]
+    L.admm_mse_f32.restype = c_int
+    L.admm_mse_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [c_void_p, c_void_p, c_size_t, c_void_p]
     L.admm_profile_enable.restype = c_int
     L.admm_profile_enable.argtypes = [c_int]
     L.admm_profile_reset.restype = c_int

@@ -28,6 +28,17 @@ namespace {
 thread_local std::string g_err;
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+}  // namespace
+
+namespace admm_internal {
+// error reporting for the other translation units of the library (metrics_capi.hip)
+int fail_msg(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace admm_internal
+
+namespace {
 int fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;

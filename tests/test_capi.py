@@ -1,4 +1,4 @@
-"""CPU: the C-ABI library loads, exports every symbol include/admm_deconv.h declares, and validates
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and validates
 arguments (no GPU compute is issued by these calls)."""
 import ctypes
 import os
@@ -8,13 +8,17 @@ import pytest
 
 from admm_deconv import _lib
 
-HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "admm_deconv.h")
+INC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HDRS = [os.path.join(INC, f) for f in ("admm_deconv.h", "admm_metrics.h")]
 
 
 def header_functions():
-    src = open(HDR).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(admm_\w+)\s*\(", src)))
+    names = set()
+    for h in HDRS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(admm_\w+)\s*\(", src))
+    names.discard("admm_reduce_fn")   # the reducer callback typedef, not an export
+    return sorted(names)
 
 
 def test_header_and_binding_agree():
