@@ -86,9 +86,9 @@ def make_inputs(cfg, B, g0, distinct, dev):
 
 def bench_c5(args, dev):
     """BASELINE c5: the denoiser branch of src/nets/net_build.jl:113-128 (5 x ADMMDeconvF2((), 50, rho, relu1)
-    in Parallel(chcat)), batch 64 of 256x256 RGB; one step = forward + MSE loss + backward through the HIP
+    in Parallel(chcat)), batch 64 of 256x256 RGB; one step = forward + GMSD loss + backward through the HIP
     adjoint + SGD update of the trainable lambda (the layers' trainable set, deconv_admm.jl:107)."""
-    from admm_deconv import layers
+    from admm_deconv import layers, metrics
     cfg = synth.CONFIGS["c5"]
     M, N, P, B, K = cfg["M"], cfg["N"], cfg["P"], args.batch or cfg["B"], cfg["K"]
     rng = np.random.default_rng(0)
@@ -105,7 +105,7 @@ def bench_c5(args, dev):
 
     def step():
         out = torch.cat([L(x) for L in branch], dim=1)        # chcat (dim 3 in Julia = channels)
-        loss = torch.mean((out - target) ** 2)
+        loss = metrics.gmsd_loss(out, target)                 # the training loss, src/train.jl:129,191
         loss.backward()
         with torch.no_grad():
             for L in branch:
@@ -136,7 +136,7 @@ def bench_c5(args, dev):
         "ms_per_step": round(1000 * el / args.steps, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
-                               "MSE, backward through admm_tvd_backward_f32 "
+                               "GMSD loss (HIP), backward through the recorded adjoint "
                                f"({'iso' if args.iso else 'aniso'})", "global_batch": B},
         "kernels": kernels}))
 
