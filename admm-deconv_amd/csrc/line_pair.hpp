@@ -104,6 +104,38 @@ __device__ __forceinline__ void fft_reg(float2 (&x)[N]) {
 template <bool INV>
 __device__ __forceinline__ void fft64_reg(float2 (&x)[64]) { fft_reg<64, INV>(x); }
 
+// fft_reg<64, INV> whose outputs 32..63 go straight to per-lane LDS slots (stg[m * 512] for m < 16,
+// stg2[(m - 16) * 512] above) as soon as their radix-16 group is final, instead of staying live:
+// the last stage otherwise needs more than 256 VGPRs and the compiler spills them to scratch.
+template <bool INV>
+__device__ __forceinline__ void fft64_reg_stage(float2 (&x)[64], float2* stg, float2* stg2) {
+    constexpr int Q = 16;
+    float2 t[Q][4];
+#pragma unroll
+    for (int n2 = 0; n2 < Q; ++n2) {
+        t[n2][0] = x[n2]; t[n2][1] = x[Q + n2]; t[n2][2] = x[2 * Q + n2]; t[n2][3] = x[3 * Q + n2];
+        dft4<INV>(t[n2][0], t[n2][1], t[n2][2], t[n2][3]);
+    }
+    sched_fence();
+    fftN_tw<64, INV, 1>(t);
+    sched_fence();
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+        float2 u[Q];
+#pragma unroll
+        for (int n2 = 0; n2 < Q; ++n2) u[n2] = t[n2][k1];
+        dft<Q, INV>(u);
+#pragma unroll
+        for (int k2 = 0; k2 < Q; ++k2) {
+            const int o = k1 + 4 * k2;
+            if (o < 32) x[o] = u[k2];
+            else if (o < 48) stg[(o - 32) * 512] = u[k2];
+            else stg2[(o - 48) * 512] = u[k2];
+        }
+        sched_fence();
+    }
+}
+
 // forward DIT combine across the pair: A: Z[k] = E[k] + W128^k O[k], B: Z[k+64] = E[k] - W128^k O[k]
 template <int K>
 __device__ __forceinline__ void combine_fwd(float2 (&x)[64], bool hb) {
@@ -210,6 +242,19 @@ __device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
     const float2 p32 = swap_pair(S[32]);
     S[32] = post_fwd<32>(S[32], p32, hb);
     post_fwd_pairs<1>(S, hb);
+}
+
+// line_inverse_pair with z registers 32..63 delivered to the LDS staging slots (fft64_reg_stage)
+__device__ __forceinline__ void line_inverse_pair_staged(float2 (&S)[64], bool hb, float2* stg, float2* stg2) {
+    const float2 x0 = S[0];
+    S[0] = hb ? make_float2(2.f * x0.x, -2.f * x0.y) : make_float2(x0.x + x0.y, x0.x - x0.y);
+    split_one<0>(S, hb);
+    const float2 p32 = swap_pair(S[32]);
+    S[32] = pre_inv<32>(S[32], p32, hb);
+    split_one<32>(S, hb);
+    pre_split_pairs<1>(S, hb);
+    sched_fence();
+    fft64_reg_stage<true>(S, stg, stg2);
 }
 
 // packed half spectrum -> z (spatial), in place (unnormalised: 256 x)

@@ -269,6 +269,9 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 // 32..63 is parked in it (per-lane slots stg[m * 512 + t]) while registers 0..31 are processed; at
 // the half-way point the slots swap x[32+m] back in and v[m] out, and v[0..30] return at the end.
 // The chunk loop thus holds ~66 S registers instead of 128.
+// STAGED: the line inverse already parked x of registers 32..63 in the staging slots
+// (line_inverse_pair_staged); S[32..63] are dead on entry.
+template <bool STAGED = false>
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sps, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho) {
@@ -286,18 +289,31 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
     float4 sor[PD + 1][CH];
     float2 hyr[PD + 1][CH];
     PLANE_STAMP(16);
-    if (bot) {
-#pragma unroll
-        for (int n = 0; n < 64; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
-    }
     // staging slots stg[m * 512 + t]: two bases keep the offsets within the 16-bit ds immediate
     float2* stg = colbuf + t;
     float2* stg2 = stg + 16 * kPT;
-    const float x63y = S[63].y;   // lane A's register 0 needs the pixel before it (B's pixel 255)
+    float x63y;   // lane A's register 0 needs the pixel before it (B's pixel 255)
+    if constexpr (STAGED) {
+        if (bot) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) stg[m * kPT] = S[32 + m];
+            for (int n = 0; n < 32; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) stg2[m * kPT] = S[48 + m];
+            for (int m = 0; m < 16; ++m) xb[(w * 2 + hb) * 64 + 32 + m] = stg[m * kPT];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) xb[(w * 2 + hb) * 64 + 48 + m] = stg2[m * kPT];
+        }
+        x63y = stg2[15 * kPT].y;
+    } else {
+        if (bot) {
+#pragma unroll
+            for (int n = 0; n < 64; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
+        }
+        x63y = S[63].y;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) stg[m * kPT] = S[32 + m];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) stg2[m * kPT] = S[48 + m];
+    }
     lds_barrier();
     // prologue loads after the staging: issued earlier they made every spill reload around the line
     // inverse wait for them (one in-order vmcnt)
@@ -428,6 +444,10 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
     }
 }
 
+#ifndef PLANE_STAGE_INV
+#define PLANE_STAGE_INV 1
+#endif
+
 // grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
 // TRAJ: record the trajectory for the adjoint -- iteration k writes s_k to slot k-1 of `traj` (slot
 // stride traj_slot float4, lane-native layout, plane p at p * 64 * 512) and reads s_{k-1} from slot
@@ -486,16 +506,30 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         if constexpr (DBG == 2) dbg_dump<DBG>(dbg, S, 256 + k, t);
         column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
-        line_inverse_pair(S, hb);
-        dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
-        if (k == K) break;
+        // the last iteration keeps x in registers for the output; the others hand x[32..63] to the
+        // row phase's LDS staging slots directly (no spill of the line inverse's peak)
+        constexpr bool kStage = DBG == 0 && PLANE_STAGE_INV;
+        if constexpr (!kStage) {
+            line_inverse_pair(S, hb);
+            dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
+            if (k == K) break;
+        } else {
+            line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
+            if (k == K) {   // the output needs x[32..63] back (per-thread slots: no barrier)
+#pragma unroll
+                for (int m = 0; m < 16; ++m) S[32 + m] = colbuf[t + m * kPT];
+#pragma unroll
+                for (int m = 0; m < 16; ++m) S[48 + m] = colbuf[t + (16 + m) * kPT];
+                break;
+            }
+        }
         if constexpr (TRAJ) {
             float4* tb = traj + plane * 64 * kPT;
             const rsrc_t sld = make_rsrc(tb + (size_t)(k >= 2 ? k - 2 : 0) * traj_slot, 64 * kPT * 16);
             const rsrc_t sst = make_rsrc(tb + (size_t)(k - 1) * traj_slot, 64 * kPT * 16);
-            row_update(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
         } else {
-            row_update(S, sp, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            row_update<kStage>(S, sp, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
         }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
         line_forward_pair(S, hb);
