@@ -18,9 +18,9 @@ ADMM_E_WORKSPACE = -3
 ADMM_E_HIP = -4
 ADMM_E_REDUCER = -5
 
-K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE = range(7)
+K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE, K_ADJ = range(8)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
-                  K_FINAL: "final", K_NORM: "norm", K_PLANE: "plane"}
+                  K_FINAL: "final", K_NORM: "norm", K_PLANE: "plane", K_ADJ: "adjoint"}
 
 # Every symbol include/admm_deconv.h declares (checked by tests/test_capi.py).
 EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "admm_tvd_forward_f32",

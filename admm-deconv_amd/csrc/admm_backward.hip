@@ -287,6 +287,24 @@ __global__ __launch_bounds__(kThreads) void hbar_corr_kernel(const float* __rest
 }
 
 // Sum column c (= blockIdx.x) of an n x w row-major matrix of per-block partials, in a fixed order.
+// first stage of a long column sum: block (c, g) sums rows [g chunk, (g + 1) chunk) of column c into
+// tmp[g w + c] (fixed partition: deterministic); reduce_cols_kernel then sums the gridDim.y partials
+__global__ __launch_bounds__(kThreads) void reduce_cols_part_kernel(const double* __restrict__ part,
+                                                                    double* __restrict__ tmp, int n, int w, int chunk) {
+    __shared__ double red[kThreads];
+    const int c = blockIdx.x, g = blockIdx.y;
+    const int i0 = g * chunk, i1 = min(n, i0 + chunk);
+    double s = 0.0;
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) s += part[(size_t)i * w + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tmp[(size_t)g * w + c] = red[0];
+}
+
 __global__ __launch_bounds__(kThreads) void reduce_cols_kernel(const double* __restrict__ part,
                                                                double* __restrict__ out, int n, int w) {
     __shared__ double red[kThreads];

@@ -657,11 +657,13 @@ struct BwdLayout {
     Layout f;
     size_t traj_s, traj_v, sig, sbA, sbB, vsum, rpart, Qp, Q, hpart, hcorr, hA, rt, total;
     size_t traj_n, wbar, Rmap, Rpart;   // isotropic only
+    size_t rtmp;                        // two-stage column sums (kRedParts x columns doubles)
     int nblk_line, nblk_corr, TY;
     int nblk_isoA, nblk_isoR;           // isotropic: per-step partial rows = nblk_isoA + nblk_isoR
 };
 
 constexpr int kIsoAdjRBlocks = 256;     // ISO_ADJ_R grid (tau_bar partial rows per step)
+constexpr int kRedParts = 256;          // first-stage blocks per column of a long column sum
 
 BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h, bool iso) {
     BwdLayout b{};
@@ -703,8 +705,23 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     b.hcorr = kh > 0 ? take((size_t)kh * kw * 8) : 0;
     b.hA = hq ? take((size_t)kh * kw * 8) : 0;
     b.rt = take(2 * 8);
+    b.rtmp = take((size_t)kRedParts * (kh * kw > 2 ? kh * kw : 2) * 8);
     b.total = off;
     return b;
+}
+
+// out[c] = sum over the n rows of column c of part (n x w row-major), in a fixed order
+void launch_reduce_cols(hipStream_t s, const double* part, double* out, int n, int w, double* tmp) {
+    const int chunk = 2048;
+    const int parts = (n + chunk - 1) / chunk;
+    if (parts <= 1) {
+        hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(w), dim3(kThreads), 0, s, part, out, n, w);
+        return;
+    }
+    const int ch = (n + (parts < kRedParts ? parts : kRedParts) - 1) / (parts < kRedParts ? parts : kRedParts);
+    const int g = (n + ch - 1) / ch;
+    hipLaunchKernelGGL(admm::reduce_cols_part_kernel, dim3(w, g), dim3(kThreads), 0, s, part, tmp, n, w, ch);
+    hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(w), dim3(kThreads), 0, s, tmp, out, g, w);
 }
 
 int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
@@ -921,7 +938,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         float* sbo = sb[(k & 1) ^ 1];
         double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
         if (!iso) {
-            rc = ln.run(ADMM_K_LINE, [&] {
+            rc = ln.run(ADMM_K_ADJ, [&] {
                 launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
                                 k == 1 ? 1 : 0, k == K ? 1 : 0, ln_traj);
             });
@@ -930,7 +947,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         }
         // isotropic: ISO_ADJ_A (plane groups) -> ISO_ADJ_R (batch R map, tau_bar) -> ISO_ADJ_B (per plane)
         const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
-        rc = ln.run(ADMM_K_LINE, [&] {
+        rc = ln.run(ADMM_K_ADJ, [&] {
             launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
                              nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, kIsoGroup, tau, rho,
                              k == 1 ? 1 : 0, k == K ? 1 : 0);
@@ -948,7 +965,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             rc = call_reducer(red, Rmap, MN, s);
             if (rc) return rc;
         }
-        rc = ln.run(ADMM_K_LINE, [&] {
+        rc = ln.run(ADMM_K_ADJ, [&] {
             launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau);
         });
         if (rc) return rc;
@@ -956,7 +973,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     // ---- assembly ----
     double* rt = reinterpret_cast<double*>(ws + bl.rt);
     rc = ln.run(ADMM_K_FINAL, [&] {
-        hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(2), dim3(kThreads), 0, s, rpart, rt, K * bl.nblk_line, 2);
+        launch_reduce_cols(s, rpart, rt, K * bl.nblk_line, 2, reinterpret_cast<double*>(ws + bl.rtmp));
     });
     if (rc) return rc;
     double* hcorr = kh > 0 ? reinterpret_cast<double*>(ws + bl.hcorr) : nullptr;
@@ -979,8 +996,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             });
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] {
-                hipLaunchKernelGGL(admm::reduce_cols_kernel, dim3(kh * kw), dim3(kThreads), 0, s, hpart, hcorr,
-                                   bl.nblk_corr, kh * kw);
+                launch_reduce_cols(s, hpart, hcorr, bl.nblk_corr, kh * kw, reinterpret_cast<double*>(ws + bl.rtmp));
             });
             if (rc) return rc;
             double* Q = reinterpret_cast<double*>(ws + bl.Q);

@@ -130,6 +130,17 @@ def bench_c5(args, dev):
         ms, n = _lib.profile_get(cls)
         if n:
             kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
+    roof = None
+    if not args.iso and "adjoint" in kernels:
+        # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1}, s_k,
+        # sbar_k, sbar_{k-1} (8 M N each) and Vsum read + write (4 M N each) -- the interior steps
+        planes = B * P
+        per_launch = planes * (16 * (M // 2) * N + 40 * M * N)
+        a = kernels["adjoint"]
+        ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": "adjoint (line_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": round(a["avg_ms"], 5)}
     print(json.dumps({
         "metric": "c5 ADMM denoiser-branch train step (fwd + adjoint) images/s", "value": round(B * args.steps / el, 2),
         "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -138,7 +149,7 @@ def bench_c5(args, dev):
         "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
                                "GMSD loss (HIP), backward through the recorded adjoint "
                                f"({'iso' if args.iso else 'aniso'})", "global_batch": B},
-        "kernels": kernels}))
+        "roofline": roof, "kernels": kernels}))
 
 
 def cpu_baseline(cfg, psf, base, target_s):

@@ -54,7 +54,8 @@ enum {
     ADMM_K_FINAL = 4,   /* last irFFT along dim1, writes x                                       */
     ADMM_K_NORM = 5,    /* isotropic only: pixelnorm over the batch (ops.jl:6)                   */
     ADMM_K_PLANE = 6,   /* fused per-plane solve, all K iterations (256 x 256, anisotropic)      */
-    ADMM_K_COUNT = 7
+    ADMM_K_ADJ = 7,     /* adjoint reverse-step line kernels (line_adj, iso_adj_a / iso_adj_b)   */
+    ADMM_K_COUNT = 8
 };
 
 /* ABI version of the loaded library (== ADMM_ABI_VERSION it was built with). */
