@@ -68,6 +68,11 @@ bool fused_enabled() {
     const char* e = getenv("ADMM_FUSED");
     return !(e && e[0] == '0');
 }
+// ADMM_FUSED_ADJ=0 keeps the 2-pass reverse sweep (line_adj + column) on a fused trajectory
+bool fused_adj_enabled() {
+    const char* e = getenv("ADMM_FUSED_ADJ");
+    return !(e && e[0] == '0');
+}
 size_t fused_tables_bytes() { return admm::plane::tables_bytes(); }
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
@@ -916,7 +921,24 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     const size_t clds = column_lds(N, KB), flds = fwdinv_lds(M, T);
     const size_t alds = line_lds(M, T) + 8 * 16;
     const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
-    HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
+    // fused reverse sweep: one workgroup per plane runs all K steps (plane256_adj_kernel)
+    const bool fused_adj = ln_traj && !iso && fused_adj_enabled();
+    int red_rows = K * bl.nblk_line;   // rows of (rho_bar, tau_bar) partials
+    if (fused_adj) {
+        namespace pk = admm::plane;
+        float4* dxK = reinterpret_cast<float4*>(sb[1]);
+        float* vout = kh > 0 ? vsum : y_bar;
+        rc = ln.run(ADMM_K_PREP, [&] { (void)pk::launch_dx_lane(xK, dxK, planes, s); });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_ADJ, [&] {
+            (void)pk::launch_plane_adj(x_bar, ws + bl.f.F, reinterpret_cast<const float4*>(tr.s), dxK,
+                                       reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, tau, rho, K, planes, s);
+        });
+        if (rc) return rc;
+        red_rows = (int)planes;
+    } else {
+        HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
+    }
     float* wbar = iso ? reinterpret_cast<float*>(ws + bl.wbar) : nullptr;
     float* Rmap = iso ? reinterpret_cast<float*>(ws + bl.Rmap) : nullptr;
     float* Rpart = iso ? reinterpret_cast<float*>(ws + bl.Rpart) : nullptr;
@@ -924,9 +946,11 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
     if (iso) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
     if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
-    rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
-    if (rc) return rc;
-    for (int k = K; k >= 1; --k) {
+    if (!fused_adj) {
+        rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
+        if (rc) return rc;
+    }
+    for (int k = fused_adj ? 0 : K; k >= 1; --k) {
         float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
             launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
@@ -973,7 +997,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     // ---- assembly ----
     double* rt = reinterpret_cast<double*>(ws + bl.rt);
     rc = ln.run(ADMM_K_FINAL, [&] {
-        launch_reduce_cols(s, rpart, rt, K * bl.nblk_line, 2, reinterpret_cast<double*>(ws + bl.rtmp));
+        launch_reduce_cols(s, rpart, rt, red_rows, 2, reinterpret_cast<double*>(ws + bl.rtmp));
     });
     if (rc) return rc;
     double* hcorr = kh > 0 ? reinterpret_cast<double*>(ws + bl.hcorr) : nullptr;
@@ -1012,7 +1036,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             });
             if (rc) return rc;
         }
-    } else {
+    } else if (!fused_adj) {   // (the fused sweep wrote Vsum straight into y_bar)
         HIPCHK(hipMemcpyAsync(y_bar, vsum, planes * MN * 4, hipMemcpyDeviceToDevice, s));
     }
     rc = ln.run(ADMM_K_FINAL, [&] {

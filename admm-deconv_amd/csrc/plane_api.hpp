@@ -29,5 +29,16 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
                         float tau, float rho, int K, size_t planes, hipStream_t s, float4* traj = nullptr);
 
+
+// Reverse sweep of the anisotropic solve on the fused trajectory (plane256_adj_kernel):
+// launch_dx_lane writes D x_K (x_K = the forward output, natural layout) in the lane-native s layout;
+// launch_plane_adj runs steps K..1 for every plane.  traj: the forward's s_1..s_{K-1}; sbar, vsl: planes x
+// 512 KiB / 256 KiB of state; vout: Vsum = sum_k vbar_k (natural layout; = y_bar without a PSF);
+// part: 2 doubles per plane (rho_bar, tau_bar partial sums, fixed summation order).
+hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s);
+hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
+                            float2* vsl, float* vout, double* part, float tau, float rho, int K, size_t planes,
+                            hipStream_t s);
+
 }  // namespace plane
 }  // namespace admm

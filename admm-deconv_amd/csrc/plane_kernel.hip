@@ -48,19 +48,33 @@ using rsrc_t = __amdgpu_buffer_rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+// cache-policy bits of the main-loop s / H^T y accesses (gfx950: 1 = sc0, 2 = nt, 16 = sc1);
+// experiment knobs, 0 = default policy
+#ifndef PLANE_AUX_LDS
+#define PLANE_AUX_LDS 0
+#endif
+#ifndef PLANE_AUX_LDH
+#define PLANE_AUX_LDH 0
+#endif
+#ifndef PLANE_AUX_ST
+#define PLANE_AUX_ST 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ float4 bld4(rsrc_t r, unsigned vo, unsigned so) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, AUX));
 }
+template <int AUX = 0>
 __device__ __forceinline__ float2 bld2(rsrc_t r, unsigned vo, unsigned so) {
-    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, AUX));
 }
 __device__ __forceinline__ float bld1(rsrc_t r, unsigned vo, unsigned so) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
 }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int AUX = 0>
 __device__ __forceinline__ void bst4(rsrc_t r, unsigned vo, unsigned so, float4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, vo, so, AUX);
 }
 __device__ __forceinline__ void bst2(rsrc_t r, unsigned vo, unsigned so, float2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
@@ -322,8 +336,8 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
     for (int g = 0; g < PD; ++g)
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            sor[g][j] = bld4(sp, t * 16, (g * CH + j) * kPT * 16);
-            hyr[g][j] = bld2(hp, t * 8, (g * CH + j) * kPT * 8);
+            sor[g][j] = bld4<PLANE_AUX_LDS>(sp, t * 16, (g * CH + j) * kPT * 16);
+            hyr[g][j] = bld2<PLANE_AUX_LDH>(hp, t * 8, (g * CH + j) * kPT * 8);
         }
     PLANE_STAMP(17);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
@@ -349,8 +363,8 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
                 __asm__ volatile("" ::"v"(sor[(g + PD) % (PD + 1)][j].x), "v"(sor[(g + PD) % (PD + 1)][j].y),
                                  "v"(sor[(g + PD) % (PD + 1)][j].z), "v"(sor[(g + PD) % (PD + 1)][j].w),
                                  "v"(hyr[(g + PD) % (PD + 1)][j].x), "v"(hyr[(g + PD) % (PD + 1)][j].y));
-                sor[(g + PD) % (PD + 1)][j] = bld4(sp, t * 16, ((g + PD) * CH + j) * kPT * 16);
-                hyr[(g + PD) % (PD + 1)][j] = bld2(hp, t * 8, ((g + PD) * CH + j) * kPT * 8);
+                sor[(g + PD) % (PD + 1)][j] = bld4<PLANE_AUX_LDS>(sp, t * 16, ((g + PD) * CH + j) * kPT * 16);
+                hyr[(g + PD) % (PD + 1)][j] = bld2<PLANE_AUX_LDH>(hp, t * 8, ((g + PD) * CH + j) * kPT * 8);
             }
         }
         if (n0 == 32) {   // half-way: x[32..63] in, v[0..30] out (x[31] still pending in S[31])
@@ -383,7 +397,7 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
 #ifndef PLANE_EXPT_NOSTORE
-            bst4(sps, t * 16, n * kPT * 16, s);
+            bst4<PLANE_AUX_ST>(sps, t * 16, n * kPT * 16, s);
 #endif
             wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
             hc[j + 1] = hyr[g % (PD + 1)][j];
@@ -538,6 +552,246 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     float2* xrow = reinterpret_cast<float2*>(x_out + plane * 65536 + (size_t)r * 256);
 #pragma unroll
     for (int n = 0; n < 64; ++n) xrow[2 * n + hb] = S[n];
+}
+
+
+// =============================================================================================
+// Fused per-plane ADJOINT (reverse sweep of the anisotropic solve): one
+// workgroup per 256 x 256 plane runs all K reverse steps with the line spectra in registers, the
+// structure of plane256_kernel run backwards (admm_backward.hip's header states the recurrences;
+// tests/kernel_model.py tvd_model_grads restates them):
+//   S = line spectra of g_K = x_bar
+//   step k = K..1:  column phase (x C/(MN): vbar_k = A^-1 g_k, A symmetric), line inverse -> vbar_k,
+//                   row phase (row_adjoint), line forward of g_{k-1} = D^T sbar_{k-1} (k >= 2)
+// HBM per pixel and step: s_{k-1}, s_k (or D x_K at k = K), sbar_k in, sbar_{k-1} out (8 B each),
+// Vsum in + out (4 B each) -- 40 B/px vs 72 for the 2-pass step (line_adj + column round trips of the
+// spectrum).  Absent operands (sbar_K, Vsum before step K, s_0, sbar_0) are buffer resources of size 0:
+// their loads return 0 and their stores are dropped, so one loop body serves every step.
+// =============================================================================================
+
+// Row phase of reverse step k.  v = vbar_k (spatial; registers 32..63 staged by the line inverse).
+//   Dvb = D vbar_k (neighbours as x in row_update);  rho_acc -= <Dvb, D x_k>, D x_k = s_k - clip(s_{k-1})
+//   (k = K: the precomputed D x_K);  Vsum += vbar_k;
+//   wbar = rho Dvb, m = |s_{k-1}| > tau:  sbar_{k-1} = m ? wbar : sbar_k - wbar,
+//   rho_acc += <phi(s_{k-1}), Dvb>,  tau_acc += m sgn(s_{k-1}) (sbar_k - 2 wbar);
+//   S <- g_{k-1} = D^T sbar_{k-1}  (finalize with H^T y = 0 and unit weight).
+// Chunks of ONE register (the ring holds 3 float4 + 1 float2 per register, 2.3x row_update's).
+#ifndef ADJX
+#define ADJX 0
+#endif
+__device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t s2p, rsrc_t sbl, rsrc_t sbs, rsrc_t vlp,
+                                            rsrc_t vsp, unsigned vso, unsigned vss, float2* xb, float2* wb,
+                                            float2* sink, float2* colbuf, int t, bool hb, bool lastk, float tau,
+                                            float rho, float& racc, float& tacc) {
+    const int lane = t & 63, w = t >> 6;
+    const bool top = lane < 2, bot = lane >= 62;
+    float4 s1r[2], s2r[2], sbr[2];
+    float2 vr[2];
+    float2* stg = colbuf + t;
+    float2* stg2 = stg + 16 * kPT;
+    if (bot) {
+#pragma unroll
+        for (int n = 0; n < 32; ++n) xb[(w * 2 + hb) * 64 + n] = S[n];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) xb[(w * 2 + hb) * 64 + 32 + m] = stg[m * kPT];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) xb[(w * 2 + hb) * 64 + 48 + m] = stg2[m * kPT];
+    }
+    const float v63y = stg2[15 * kPT].y;
+    lds_barrier();
+    sched_fence();
+    s1r[0] = bld4(s1p, t * 16, 0);
+    s2r[0] = bld4(s2p, t * 16, 0);
+    sbr[0] = bld4(sbl, t * 16, 0);
+    vr[0] = bld2(vlp, t * 8, 0);
+    const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
+    float2* wbm = top ? wb + (w * 2 + hb) * 64 : sink + w * 128 + lane;
+    float4 wc[2];
+    float w2x0 = 0.0f;
+    const float2 zero2 = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+        if (n + 1 < 64) {
+            const int q = (n + 1) & 1;
+            __asm__ volatile("" ::"v"(s1r[q].x), "v"(s1r[q].y), "v"(s1r[q].z), "v"(s1r[q].w), "v"(s2r[q].x),
+                             "v"(s2r[q].y), "v"(s2r[q].z), "v"(s2r[q].w));
+            __asm__ volatile("" ::"v"(sbr[q].x), "v"(sbr[q].y), "v"(sbr[q].z), "v"(sbr[q].w), "v"(vr[q].x),
+                             "v"(vr[q].y));
+            if (!(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + 1) * kPT * 16);
+            if (!(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + 1) * kPT * 16);
+            if (!(ADJX & 4)) sbr[q] = bld4(sbl, t * 16, (n + 1) * kPT * 16);
+            if (!(ADJX & 2)) vr[q] = bld2(vlp, t * 8, (n + 1) * kPT * 8);
+        }
+        if (n == 32) {   // half-way: vbar[32..63] in, g[0..30] out (vbar[31] still pending in S[31])
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const float2 xv = stg[m * kPT];
+                stg[m * kPT] = S[m];
+                S[32 + m] = xv;
+            }
+#pragma unroll
+            for (int m = 0; m < 15; ++m) {
+                const float2 xv = stg2[m * kPT];
+                stg2[m * kPT] = S[16 + m];
+                S[48 + m] = xv;
+            }
+            S[63] = stg2[15 * kPT];
+            sched_fence();
+        }
+        const float4 s1 = s1r[n & 1], s2 = s2r[n & 1], sb = sbr[n & 1];
+        const float2 vo = vr[n & 1];
+        const float2 v = S[n];
+        const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
+        const float2 vub = xbp[n];
+        float2 vu = make_float2(__shfl_up(v.x, 2), __shfl_up(v.y, 2));
+        vu.x = top ? vub.x : vu.x;
+        vu.y = top ? vub.y : vu.y;
+        const float dv[4] = {v.x - vu.x, v.y - vu.y, v.x - vl, v.y - v.x};
+        const float a1[4] = {s1.x, s1.y, s1.z, s1.w}, a2[4] = {s2.x, s2.y, s2.z, s2.w};
+        const float b[4] = {sb.x, sb.y, sb.z, sb.w};
+        float nb[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float dx = lastk ? a2[c] : a2[c] - clip_tau(a1[c], tau);
+            racc -= dv[c] * dx;
+            const float wbv = rho * dv[c];
+            const bool m = fabsf(a1[c]) > tau;
+            nb[c] = m ? wbv : b[c] - wbv;
+            racc += phi_tau(a1[c], tau) * dv[c];
+            const float sg = (a1[c] > 0.f) ? 1.0f : -1.0f;
+            tacc += m ? sg * (b[c] - 2.0f * wbv) : 0.0f;
+        }
+        // pin the accumulators here: left free, the compiler sinks the sums to the end of the
+        // unrolled loop and keeps every register's operands live until then (~2000 VGPRs of spills)
+        __asm__ volatile("" : "+v"(racc), "+v"(tacc));
+        if (!(ADJX & 2)) bst2(vsp, vso, n * vss, make_float2(vo.x + v.x, vo.y + v.y));
+        const float4 nb4 = make_float4(nb[0], nb[1], nb[2], nb[3]);
+        bst4(sbs, t * 16, n * kPT * 16, nb4);
+        wbm[n] = make_float2(nb4.x, nb4.y);
+        if (n == 0) {
+            w2x0 = nb4.z;
+        } else {
+            S[n - 1] = finalize(wc[(n - 1) & 1], nb4, zero2, hb, bot, 1.0f);
+        }
+        wc[n & 1] = nb4;
+        sched_fence();
+    }
+    S[63] = finalize(wc[1], make_float4(0.f, 0.f, w2x0, 0.f), zero2, hb, bot, 1.0f);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) S[m] = stg[m * kPT];
+#pragma unroll
+    for (int m = 0; m < 15; ++m) S[16 + m] = stg2[m * kPT];
+    lds_barrier();
+    if (bot) {
+        const float2* wbn = wb + (((w + 1) & 7) * 2 + hb) * 64;   // next wave's first line
+#pragma unroll
+        for (int n = 0; n < 64; ++n) {
+            const float2 a = wbn[n];
+            S[n].x -= a.x;
+            S[n].y -= a.y;
+        }
+    }
+}
+
+// D x_K in the lane-native s layout (entry [n][t] = (d0[p], d0[p+1], d1[p], d1[p+1]) of pixel pair
+// p = 4n + 2h of line r, t = 2r + h): the reverse sweep's step-K operand.  grid (128, planes) x 256.
+__global__ __launch_bounds__(256) void dx_lane_kernel(const float* __restrict__ x, float4* __restrict__ out) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;   // [n][t]
+    const int n = idx >> 9, t = idx & 511;
+    const int r = t >> 1, p = 4 * n + 2 * (t & 1);
+    const float* xp = x + (size_t)blockIdx.y * 65536;
+    const float2 c = *reinterpret_cast<const float2*>(xp + r * 256 + p);
+    const float2 u = *reinterpret_cast<const float2*>(xp + ((r + 255) & 255) * 256 + p);
+    const float l = xp[r * 256 + ((p + 255) & 255)];
+    out[(size_t)blockIdx.y * 64 * kPT + idx] = make_float4(c.x - u.x, c.y - u.y, c.x - l, c.y - c.x);
+}
+
+// grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
+//   xbar    : upstream gradient of x_K (natural layout)        traj : s_1..s_{K-1}, plane256_kernel<., ., true>
+//   dxK     : D x_K (dx_lane_kernel)                           sbar : lane-native sbar state (in place)
+//   vsl     : lane-native Vsum accumulator                     vout : Vsum = sum_k vbar_k, natural layout
+//   part    : per plane (rho_bar partial, tau_bar partial) in fp64
+__global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restrict__ xbar, const float* __restrict__ Cf,
+                                                           const float* __restrict__ C0b,
+                                                           const float4* __restrict__ traj, size_t traj_slot,
+                                                           const float4* __restrict__ dxK, float4* __restrict__ sbar,
+                                                           float2* __restrict__ vsl, float* __restrict__ vout,
+                                                           double* __restrict__ part, float tau, float rho, int K) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* colbuf = reinterpret_cast<float2*>(smem_raw);
+    float2* tw = colbuf + kColF2;
+    float2* xb = tw + kTwF2;
+    float2* wb = xb + kBndF2;
+    float2* sink = wb + kBndF2;
+    float2* mir = sink;
+    const int t = threadIdx.x;
+    float* c0l = reinterpret_cast<float*>(sink + kDumF2);
+    if (t < 256) c0l[t] = C0b[t];
+    const bool hb = t & 1;
+    const int r = t >> 1;
+    const size_t plane = blockIdx.x;
+    if (t < 256) {
+        const int q = t >> 5, k = t & 31;
+        double sn, cs;
+        sincospi((double)(q * k) / 128.0, &sn, &cs);
+        tw[q * kTQ + k] = make_float2((float)cs, (float)-sn);
+    }
+    const float2* grow = reinterpret_cast<const float2*>(xbar + plane * 65536 + (size_t)r * 256);
+    float2 S[64];
+#pragma unroll
+    for (int n = 0; n < 64; ++n) S[n] = grow[2 * n + hb];
+    const rsrc_t cfr = make_rsrc(Cf, kTab * 4);
+    const rsrc_t none = make_rsrc(Cf, 0);
+    constexpr unsigned kS4 = 64 * kPT * 16, kS2 = 64 * kPT * 8;
+    const float4* tb = traj + plane * 64 * kPT;
+    float4* sbp = sbar + plane * 64 * kPT;
+    float2* vlp = vsl + plane * 64 * kPT;
+    double rsum = 0.0, tsum = 0.0;
+    line_forward_pair(S, hb);
+    for (int k = K;; --k) {
+        column_half<0, 0>(S, colbuf, tw, mir, cfr, c0l, none, nullptr, t, hb);
+        column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, none, nullptr, t, hb);
+        line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
+        const rsrc_t s1p = k >= 2 ? make_rsrc(tb + (size_t)(k - 2) * traj_slot, kS4) : none;
+        const rsrc_t s2p = k == K ? make_rsrc(dxK + plane * 64 * kPT, kS4) : make_rsrc(tb + (size_t)(k - 1) * traj_slot, kS4);
+        const rsrc_t sbl = k < K ? make_rsrc(sbp, kS4) : none;
+        const rsrc_t sbs = k >= 2 ? make_rsrc(sbp, kS4) : none;
+        const rsrc_t vlr = k < K ? make_rsrc(vlp, kS2) : none;
+        // the last step writes Vsum in the natural layout: byte r * 1024 + 16 n + 8 h
+        const rsrc_t vsr = k >= 2 ? make_rsrc(vlp, kS2) : make_rsrc(vout + plane * 65536, 65536 * 4);
+        const unsigned vso = k >= 2 ? (unsigned)t * 8 : (unsigned)(r * 1024 + hb * 8);
+        const unsigned vss = k >= 2 ? kPT * 8 : 16;
+        float racc = 0.0f, tacc = 0.0f;
+#if !(ADJX & 1)
+        row_adjoint(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
+                    tacc);
+#endif
+        rsum += racc;
+        tsum += tacc;
+        if (k == 1) break;
+        line_forward_pair(S, hb);
+    }
+    // block sums in a fixed order
+    for (int off = 32; off > 0; off >>= 1) {
+        rsum += __shfl_down(rsum, off);
+        tsum += __shfl_down(tsum, off);
+    }
+    double* red = reinterpret_cast<double*>(colbuf);
+    lds_barrier();
+    if ((t & 63) == 0) {
+        red[2 * (t >> 6)] = rsum;
+        red[2 * (t >> 6) + 1] = tsum;
+    }
+    lds_barrier();
+    if (t == 0) {
+        double a = 0.0, b = 0.0;
+        for (int i = 0; i < kPT / 64; ++i) {
+            a += red[2 * i];
+            b += red[2 * i + 1];
+        }
+        part[2 * plane] = a;
+        part[2 * plane + 1] = b;
+    }
 }
 
 }  // namespace plane

@@ -59,5 +59,22 @@ hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool p
     return hipGetLastError();
 }
 
+
+hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s) {
+    hipLaunchKernelGGL(dx_lane_kernel, dim3(64 * kPT / 256, (unsigned)planes), dim3(256), 0, s, xK, dxK);
+    return hipGetLastError();
+}
+
+hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
+                            float2* vsl, float* vout, double* part, float tau, float rho, int K, size_t planes,
+                            hipStream_t s) {
+    const Tables t = carve(tables);
+    (void)hipFuncSetAttribute((const void*)plane256_adj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kLdsBytes);
+    hipLaunchKernelGGL(plane256_adj_kernel, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf, t.C0b, traj,
+                       planes * 64 * kPT, dxK, sbar, vsl, vout, part, tau, rho, K);
+    return hipGetLastError();
+}
+
 }  // namespace plane
 }  // namespace admm

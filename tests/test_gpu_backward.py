@@ -191,3 +191,56 @@ def test_record_then_backward_equals_combined(dev, case):
         assert torch.equal(hb, hb2)
     with pytest.raises(RuntimeError):
         admm_deconv.tvd_fft_backward_recorded(rec, x, xb)
+
+
+FUSED_ADJ_CASES = [
+    # (B, P, psf, lam, rho, K)
+    (2, 1, None, 0.0041, 0.021, 1),
+    (1, 2, None, 0.05, 0.02, 2),
+    (3, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 3),
+    (2, 1, ("gauss", 9, 1.5), 0.01, 0.05, 12),
+    (1, 3, None, 0.0041, 0.021, 50),   # c5 layer shape: RGB, no PSF, K=50
+]
+
+
+@pytest.mark.parametrize("case", FUSED_ADJ_CASES,
+                         ids=[f"{c[0]}x{c[1]}-{'psf' if c[2] else 'nopsf'}-K{c[5]}" for c in FUSED_ADJ_CASES])
+def test_backward_fused_adjoint(dev, case, monkeypatch):
+    """256 x 256 anisotropic, no h_bar: the reverse sweep runs in plane256_adj_kernel (one workgroup per
+    plane, all K steps).  Against the fp64 oracle, and against the 2-pass reverse sweep over the SAME
+    recorded trajectory (ADMM_FUSED_ADJ=0: same ST masks, so only fp32 rounding separates the two)."""
+    B, P, spec, lam, rho, K = case
+    rng = np.random.default_rng(K + 17 * B)
+    h = psf(spec, rng)
+    y = synth.make_batch(B, 256, 256, h, P=P, g0=21)
+    xbar = rng.standard_normal(y.shape).astype(np.float32)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
+    x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
+    yb, _, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt)
+    x_, rec2 = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
+    monkeypatch.setenv("ADMM_FUSED_ADJ", "0")
+    yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward_recorded(rec2, x_, xt)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x_)
+    yb_, yb2_ = yb.cpu().numpy(), yb2.cpu().numpy()
+    assert_grad(yb_, yb2_, "y_bar fused vs 2-pass adjoint", trim=0.0, tol=1e-5, full_tol=1e-5)
+    assert rel(float(lb), float(lb2)) < 1e-4 and rel(float(rb), float(rb2)) < 1e-4, (lb, lb2, rb, rb2)
+    x0, yb0, _, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
+                                                      None if h is None else h.astype(np.float64), False, K, xbar)
+    assert_parity(x.cpu().numpy(), x0, what="x")
+    assert_grad(yb_, yb0, "y_bar")
+    assert rel(float(lb), lb0) < 1e-2 and rel(float(rb), rb0) < 1e-2
+
+
+def test_backward_fused_adjoint_deterministic(dev):
+    h = synth.gaussian_psf(15, 2.5)
+    y = torch.from_numpy(synth.make_batch(4, 256, 256, h)).to(dev)
+    xb = torch.randn_like(y)
+    ht = torch.from_numpy(h).to(dev)
+    a = admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, ht, False, 25, need_h=False)
+    b = admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, ht, False, 25, need_h=False)
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        if u is not None:
+            assert torch.equal(u, v)
