@@ -23,8 +23,8 @@ import torch
 
 from .ops import tvd_fft
 
-__all__ = ["ADMMDeconv", "ADMMDeconvF1", "ADMMDeconvF2", "ADMMDeconvF3", "Admm", "glorot_uniform",
-           "identity", "relu", "relu6", "relu1"]
+__all__ = ["ADMMDeconv", "ADMMDeconvF1", "ADMMDeconvF2", "ADMMDeconvF3", "Admm", "Parallel", "chcat",
+           "glorot_uniform", "identity", "relu", "relu6", "relu1"]
 
 
 def identity(x):
@@ -104,16 +104,22 @@ class Admm:
             self.bias = self.bias.to(dev)
         return self
 
-    def __call__(self, x):
-        """(d::Admm)(x) -- deconv_admm.jl:215-225."""
-        # projection written back into the layer (deconv_admm.jl:216-219); in place on the leaf
-        # parameters so that, like Zygote on the reference, gradients reach the stored tensors
+    def project(self):
+        """The projection the forward writes back into the layer (deconv_admm.jl:216-219); in place on
+        the leaf parameters so that, like Zygote on the reference, gradients reach the stored tensors."""
         with torch.no_grad():
             self.lam.clamp_(min=self.creg)                       # :216
             self.rho.clamp_(min=self.creg)                       # :217
             self.weight.clamp_(0.0, 1.0)                         # :219
+
+    def __call__(self, x, scalars=None):
+        """(d::Admm)(x) -- deconv_admm.jl:215-225.  scalars: host (lambda, rho) of the already projected
+        layer (Parallel reads every branch's pair with one device-to-host copy); None = project and
+        read them here."""
+        if scalars is None:
+            self.project()
         h = self.weight if self.weight.numel() > 0 else None
-        res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters, group=self.group)   # :221
+        res = tvd_fft(x, self.lam, self.rho, h, self.iso, self.iters, group=self.group, scalars=scalars)   # :221
         if self.bias is not False:
             res = res + self.bias                                 # :222
         return self.sigma(res)                                    # :224
@@ -190,3 +196,71 @@ class ADMMDeconvF3(Admm):
         rng = rng if rng is not None else np.random.default_rng()
         w = _psf(tuple(k), init, groups, rng)
         super().__init__(sigma, w, _bias(bias), [lam], [rho], num_it, iso, creg, device)
+
+
+def chcat(*xs):
+    """chcat(x...) = cat(x..., dims=3) (src/nets/net_build.jl:6): the channel axis, torch dim 1."""
+    return torch.cat(xs, dim=1)
+
+
+class Parallel:
+    """Flux `Parallel(connection, layers...)` as the nets build it (net_build.jl:121-125, :175): every
+    branch sees the same input and `connection` combines the branch outputs.
+
+    The branches are independent, so on a ROCm device each runs on its own HIP stream (forward, and --
+    autograd replays a backward op on its forward's stream -- the adjoint too), then the caller's stream
+    waits for all of them.  One ADMM layer's per-plane kernels occupy one CU per plane (192 of 256 CUs
+    for the c5 batch of 64 RGB images); concurrent branches fill the rest.  streams=False runs the
+    branches one after the other on the caller's stream (the reference's single task-local stream)."""
+
+    def __init__(self, connection, *layers, streams=True):
+        self.connection = connection
+        self.layers = list(layers)
+        self.use_streams = bool(streams)
+        self._streams = {}
+
+    def _side_streams(self, dev):
+        if dev not in self._streams:
+            self._streams[dev] = [torch.cuda.Stream(device=dev) for _ in self.layers]
+        return self._streams[dev]
+
+    def __call__(self, x):
+        if not (self.use_streams and isinstance(x, torch.Tensor) and x.is_cuda and len(self.layers) > 1):
+            return self.connection(*[L(x) for L in self.layers])
+        cur = torch.cuda.current_stream(x.device)
+        side = self._side_streams(x.device)
+        # project every ADMM branch and read all (lambda, rho) pairs with ONE device-to-host copy: the
+        # C ABI takes them by value, and a per-branch read would block the host behind the branches
+        # already queued
+        adm = [isinstance(L, Admm) for L in self.layers]
+        host = None
+        if any(adm):
+            for L, a in zip(self.layers, adm):
+                if a:
+                    L.project()
+            host = torch.cat([torch.cat([L.lam.detach().reshape(1), L.rho.detach().reshape(1)])
+                              for L, a in zip(self.layers, adm) if a]).cpu().tolist()
+        outs = []
+        i = 0
+        for L, a, st in zip(self.layers, adm, side):
+            x.record_stream(st)     # read on st (forward, and by the adjoint on st after the join)
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                if a:
+                    outs.append(L(x, scalars=(host[2 * i], host[2 * i + 1])))
+                    i += 1
+                else:
+                    outs.append(L(x))
+        for o, st in zip(outs, side):
+            cur.wait_stream(st)
+            o.record_stream(cur)    # allocated on st, consumed on the caller's stream
+        return self.connection(*outs)
+
+    def __getitem__(self, i):
+        return self.layers[i]
+
+    def __len__(self):
+        return len(self.layers)
+
+    def __repr__(self):
+        return f"Parallel({getattr(self.connection, '__name__', self.connection)}, {', '.join(map(repr, self.layers))})"

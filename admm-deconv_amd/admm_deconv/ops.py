@@ -276,10 +276,11 @@ class _TvdFFTFn(torch.autograd.Function):
     (the rrule the Julia shim would register, julia/ADMMDeconvHIP.jl)."""
 
     @staticmethod
-    def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit, group):
+    def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit, group, scalars):
         # the forward records its trajectory; the backward runs only the reverse sweep from it
         need_h = h_t.numel() > 0 and ctx.needs_input_grad[3]
-        x, ctx.rec = tvd_fft_record(y, lam_t, rho_t, h_t if h_t.numel() else None, isotropic, maxit,
+        lam, rho = scalars if scalars is not None else (lam_t, rho_t)
+        x, ctx.rec = tvd_fft_record(y, lam, rho, h_t if h_t.numel() else None, isotropic, maxit,
                                     need_h=need_h, group=group)
         ctx.save_for_backward(lam_t, rho_t, h_t, x)   # x: version-checked (must stay unmodified)
         return x
@@ -296,11 +297,11 @@ class _TvdFFTFn(torch.autograd.Function):
         return (yb if ctx.needs_input_grad[0] else None,
                 lb.reshape(lam_t.shape).to(lam_t.dtype) if ctx.needs_input_grad[1] else None,
                 rb.reshape(rho_t.shape).to(rho_t.dtype) if ctx.needs_input_grad[2] else None,
-                hg, None, None, None)
+                hg, None, None, None, None)
 
 
 def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None,
-            group=None):
+            group=None, scalars=None):
     """ADMM TV deconvolution of every (M x N) plane of y -- src/ops/ops.jl:181 semantics.
 
     y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: scalars or
@@ -310,11 +311,15 @@ def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, wo
     group: torch.distributed group the batch is sharded over (each rank passes its own slice).  The
     isotropic prox's pixelnorm then spans the whole sharded batch (one M x N all-reduce per
     iteration), so every rank gets its slice of the unsharded result; ignored for the anisotropic
-    prox, whose planes are independent."""
+    prox, whose planes are independent.
+    scalars: optional host (lambda, rho) equal to the values of tensor lam / rho, so that the call does
+    not read them back from the device (a host sync); gradients still flow to the tensors."""
     tensors = [t for t in (y, lam, rho, h) if isinstance(t, torch.Tensor)]
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
         dev = y.device
         as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.tensor([float(v)], device=dev)  # noqa: E731
         h_t = h if isinstance(h, torch.Tensor) else torch.zeros(0, device=dev)
-        return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit), group)
+        return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit), group, scalars)
+    if scalars is not None:
+        lam, rho = scalars
     return _forward_raw(y, lam, rho, h, isotropic, maxit, out=out, workspace=workspace, stream=stream, group=group)

@@ -64,3 +64,26 @@ def test_creg_clamp(dev):
     L = layers.ADMMDeconvF3((5, 5), 3, 0.001, 0.002, creg=0.01, device=dev)
     L(torch.from_numpy(synth.make_batch(1, 32, 32, None)).to(dev))
     assert abs(L.lam.item() - 0.01) < 1e-7 and abs(L.rho.item() - 0.01) < 1e-7
+
+
+def test_parallel_branches_on_streams_match_serial(dev):
+    """Parallel(chcat, ...) (net_build.jl:121-125) with every branch on its own HIP stream gives the same
+    forward output and the same parameter / input gradients, bitwise, as the branches run serially."""
+    from admm_deconv import layers
+    x0 = torch.from_numpy(synth.make_batch(3, 256, 256, None, P=3, sigma=0.1)).to(dev)
+    grads = []
+    for streams in (True, False):
+        rng = np.random.default_rng(5)
+        branch = [layers.ADMMDeconvF2((), 12, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.2, 4.0)]
+        for L in branch:
+            L.lam.requires_grad_(True)
+        net = layers.Parallel(layers.chcat, *branch, streams=streams)
+        x = x0.clone().requires_grad_(True)
+        out = net(x)
+        (out * torch.linspace(0, 1, out.shape[1], device=dev).reshape(1, -1, 1, 1)).sum().backward()
+        torch.cuda.synchronize()
+        grads.append((out.detach(), x.grad, [L.lam.grad for L in branch]))
+    (o1, g1, l1), (o2, g2, l2) = grads
+    assert o1.shape == (3, 9, 256, 256)
+    assert torch.equal(o1, o2) and torch.equal(g1, g2)
+    assert all(torch.equal(a, b) for a, b in zip(l1, l2))
