@@ -130,10 +130,14 @@ def bench_c5(args, dev):
         step()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    # per-kernel timing from a separate instrumented step with the branches serialised, so that each
+    # launch's hipEvent duration is its own (concurrent branches share the CUs)
+    net.use_streams = False
     _lib.profile_reset()
     _lib.profile_enable(True)
     step()
     _lib.profile_enable(False)
+    net.use_streams = not args.serial_branches
     kernels = {}
     for cls, name in _lib.KERNEL_CLASSES.items():
         ms, n = _lib.profile_get(cls)
@@ -149,7 +153,7 @@ def bench_c5(args, dev):
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "adjoint (plane256_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("c5", "adjoint"),
                 "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": round(a["avg_ms"], 5)}
     elif not args.iso and "adjoint" in kernels:
         # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1}, s_k,

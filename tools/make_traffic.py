@@ -20,6 +20,8 @@ CLASS = {"line_kernel": "line", "column_kernel<256, false>": "column", "iso_a_ke
 def klass(name):
     if "plane256_kernel" in name:
         return "plane"
+    if "plane256_adj_kernel" in name:
+        return "adjoint"
     for k, v in CLASS.items():
         if name.startswith(k):
             return v
