@@ -541,13 +541,16 @@ __global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __rest
                                                              const float* __restrict__ nrm1, int ngroups, size_t MN,
                                                              float tau, double* __restrict__ part) {
     __shared__ double red[2 * (kThreads / 64)];
+    __shared__ float gred[kThreads];
     float tacc = 0.0f;
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
-        float R = 0.0f;
-        for (int g = 0; g < ngroups; ++g) R += rpartial[(size_t)g * MN + q];
-        Rmap[q] = R;
-        const float nn = nrm1[q];
-        if (nn > tau) tacc -= R / nn;
+    for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
+        const size_t q = base + (threadIdx.x & 63);
+        const float R = group_sum(rpartial, ngroups, MN, q, gred);   // group_sum: admm_kernels.hip
+        if (threadIdx.x < 64 && q < MN) {
+            Rmap[q] = R;
+            const float nn = nrm1[q];
+            if (nn > tau) tacc -= R / nn;
+        }
     }
     block_sum2(0.0f, tacc, part + 2 * blockIdx.x, red);
 }

@@ -77,7 +77,15 @@ size_t fused_tables_bytes() { return admm::plane::tables_bytes(); }
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
-constexpr int kIsoGroup = 16;   // planes per ISO_A block (partial batch-norm sums)
+// Planes per isotropic plane-group block (ISO_A / ISO_ADJ_A keep a group's partial batch sums in
+// registers; ISO_R / ISO_ADJ_R add the groups' maps).  At most 64 groups: enough blocks to fill the chip
+// (64 x N/T), while the group maps stay small (64 x M x N floats).  16 planes per group for every batch
+// left the c5 batch (192 planes) at 12 x 32 = 384 blocks, a block and a half per CU.
+int iso_group(size_t planes) { return (int)((planes + 63) / 64); }
+int iso_ngroups(size_t planes) {
+    const int g = iso_group(planes);
+    return (int)((planes + g - 1) / g);
+}
 
 Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     Layout L{};
@@ -101,7 +109,7 @@ Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.spec1 = take(spec_bytes);
     L.xg = generic_shape(M, N) ? take(planes * MN * 4) : 0;
     L.fmap = iso ? take(MN * 4) : 0;
-    L.part = iso ? take(((planes + kIsoGroup - 1) / kIsoGroup) * MN * 4) : 0;
+    L.part = iso ? take((size_t)iso_ngroups(planes) * MN * 4) : 0;
     L.F = fused_shape(M, N, iso) ? take(fused_tables_bytes()) : 0;
     L.total = off;
     return L;
@@ -506,13 +514,13 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 sn = tr.s + (size_t)(it - 1) * sstride;
             }
             float* nrm_out = tr.nrm ? tr.nrm + (size_t)(it - 1) * MN : nullptr;
-            const int ng = (int)((np + kIsoGroup - 1) / kIsoGroup);
+            const int ng = iso_ngroups(np);
             rc = ln.run(ADMM_K_LINE, [&] {
                 launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, so, sn, fmap, part, twM, N, (int)np,
-                             kIsoGroup, it == 1 ? 1 : 0);
+                             iso_group(np), it == 1 ? 1 : 0);
             });
             if (rc) return rc;
-            const int nb = (int)((MN + kThreads - 1) / kThreads);
+            const int nb = (int)((MN + 63) / 64);   // 64 pixels per block (group_sum)
             const dim3 gr(nb < 2048 ? nb : 2048);
             if (red) {
                 // sharded batch: per-shard sum -> caller's all-reduce -> BT factor
@@ -588,7 +596,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, hty, spec0, twM, pM, N, T); });
         if (rc) return rc;
     }
-    const int ng = (int)((planes + kIsoGroup - 1) / kIsoGroup);
+    const int ng = iso_ngroups(planes);
     for (int it = 1; it <= maxit; ++it) {
         rc = ln.run(ADMM_K_COLUMN, [&] {
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 0, 1.0f);
@@ -613,10 +621,10 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         float* sa = sbuf[0];
         rc = ln.run(ADMM_K_LINE, [&] {
             hipLaunchKernelGGL(g::iso_a_kernel, dim3(N / T, ng), dim3(256), (size_t)T * M * 4, s, xg, sa, fmap, part, M,
-                               N, (int)planes, kIsoGroup, T, it == 1 ? 1 : 0);
+                               N, (int)planes, iso_group(planes), T, it == 1 ? 1 : 0);
         });
         if (rc) return rc;
-        const int nb = (int)((MN + kThreads - 1) / kThreads);
+        const int nb = (int)((MN + 63) / 64);   // 64 pixels per block (group_sum)
         const dim3 gr(nb < 2048 ? nb : 2048);
         if (red) {
             rc = ln.run(ADMM_K_NORM, [&] {
@@ -690,7 +698,7 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     b.sbB = take(planes * 2 * MN * 4);
     b.vsum = take(planes * MN * 4);
     if (iso) {
-        const size_t ng = (planes + kIsoGroup - 1) / kIsoGroup;
+        const size_t ng = iso_ngroups(planes);
         b.traj_n = take((size_t)(K > 1 ? K - 1 : 1) * MN * 4);
         b.wbar = take(planes * 2 * MN * 4);
         b.Rmap = take(MN * 4);
@@ -942,7 +950,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     float* wbar = iso ? reinterpret_cast<float*>(ws + bl.wbar) : nullptr;
     float* Rmap = iso ? reinterpret_cast<float*>(ws + bl.Rmap) : nullptr;
     float* Rpart = iso ? reinterpret_cast<float*>(ws + bl.Rpart) : nullptr;
-    const int ngi = (int)((planes + kIsoGroup - 1) / kIsoGroup);
+    const int ngi = iso_ngroups(planes);
     // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
     if (iso) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
     if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
@@ -973,7 +981,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
         rc = ln.run(ADMM_K_ADJ, [&] {
             launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
-                             nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, kIsoGroup, tau, rho,
+                             nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, iso_group(planes), tau, rho,
                              k == 1 ? 1 : 0, k == K ? 1 : 0);
         });
         if (rc) return rc;

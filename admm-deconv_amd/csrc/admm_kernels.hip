@@ -717,14 +717,36 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
 }
 
 // nrm_out (optional) keeps the per-pixel batch norm for the adjoint (trajectory recording)
+// Sum over the plane groups' maps at pixels base .. base+63: a block = 64 pixels x 4 group slices (slice
+// s adds groups s, s+4, ...; 16 loads in flight per thread at 64 groups instead of 64 dependent ones),
+// slices combined in a fixed order (deterministic).  The result is valid on slice 0 (threads 0..63).
+__device__ __forceinline__ float group_sum(const float* __restrict__ part, int ngroups, size_t MN, size_t q,
+                                           float* red) {
+    const int slice = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float a = 0.0f;
+    if (q < MN) {
+#pragma unroll 4
+        for (int g = slice; g < ngroups; g += 4) a += part[(size_t)g * MN + q];
+    }
+    red[threadIdx.x] = a;
+    __syncthreads();
+    float r = 0.0f;
+    if (slice == 0) r = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+    __syncthreads();
+    return r;
+}
+
 __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
                                                          int ngroups, size_t MN, float tau, float* __restrict__ nrm_out) {
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
-        float acc = 0.0f;
-        for (int g = 0; g < ngroups; ++g) acc += part[(size_t)g * MN + q];
-        const float nrm = sqrtf(acc);
-        fmap[q] = max0_nan(1.0f - tau / nrm);   // BT factor, ops.jl:10
-        if (nrm_out) nrm_out[q] = nrm;
+    __shared__ float red[kThreads];
+    for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
+        const size_t q = base + (threadIdx.x & 63);
+        const float acc = group_sum(part, ngroups, MN, q, red);
+        if (threadIdx.x < 64 && q < MN) {
+            const float nrm = sqrtf(acc);
+            fmap[q] = max0_nan(1.0f - tau / nrm);   // BT factor, ops.jl:10
+            if (nrm_out) nrm_out[q] = nrm;
+        }
     }
 }
 
@@ -732,10 +754,11 @@ __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict
 // all-reduce of that M x N map, and the BT factor
 __global__ __launch_bounds__(kThreads) void iso_sum_kernel(const float* __restrict__ part, float* __restrict__ acc,
                                                            int ngroups, size_t MN) {
-    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
-        float a = 0.0f;
-        for (int g = 0; g < ngroups; ++g) a += part[(size_t)g * MN + q];
-        acc[q] = a;
+    __shared__ float red[kThreads];
+    for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
+        const size_t q = base + (threadIdx.x & 63);
+        const float a = group_sum(part, ngroups, MN, q, red);
+        if (threadIdx.x < 64 && q < MN) acc[q] = a;
     }
 }
 
