@@ -266,7 +266,9 @@ __global__ __launch_bounds__(kThreads) void hbar_corr_kernel(const float* __rest
     for (int idx = threadIdx.x; idx < TY * M; idx += blockDim.x) Vt[idx] = vp[(size_t)j0 * M + idx];
     for (int idx = threadIdx.x; idx < (TY + kw - 1) * M; idx += blockDim.x) {
         const int r = idx / M, i = idx - r * M;
-        Yt[idx] = yp[(size_t)((j0 - padr + r) & (N - 1)) * M + i];
+        int jj = (j0 - padr + r) % N;   // any N (the runtime-length path too); kw <= N
+        jj += jj < 0 ? N : 0;
+        Yt[idx] = yp[(size_t)jj * M + i];
     }
     __syncthreads();
     const int ntaps = kh * kw;
@@ -278,7 +280,10 @@ __global__ __launch_bounds__(kThreads) void hbar_corr_kernel(const float* __rest
         float acc = 0.0f;
         for (int p = lane; p < TY * M; p += 64) {
             const int t = p / M, i = p - t * M;
-            acc += Vt[p] * Yt[(t + b) * M + ((i + a - padd) & (M - 1))];
+            int ii = i + a - padd;   // in (-M, 2M) for kh <= M
+            ii += ii < 0 ? M : 0;
+            ii -= ii >= M ? M : 0;
+            acc += Vt[p] * Yt[(t + b) * M + ii];
         }
         double d = acc;
         for (int off = 32; off > 0; off >>= 1) d += __shfl_down(d, off);
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(kThreads) void hbarA_kernel(const double* __restric
         const double2 S = SigT[q];
         const double dS = 2.0 * (S.x * c + S.y * s);    // 2 Re(conj(Sigma) e^{-i th})
         const double Cm = (double)Ct[q] * (double)M * (double)N;   // Ct holds C/(MN)
-        const double wk = (k == 0 || k == L) ? 1.0 : 2.0;
+        const double wk = (k == 0 || 2 * k == M) ? 1.0 : 2.0;   // self-conjugate bins (M odd: bin 0 only)
         acc += wk * Cm * Cm * Q[q] * dS;
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);

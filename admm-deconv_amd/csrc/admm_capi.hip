@@ -21,6 +21,7 @@
 #include "admm_kernels.hip"
 #include "admm_generic.hip"
 #include "admm_backward.hip"
+#include "admm_generic_bwd.hip"
 #include "plane_api.hpp"
 
 namespace {
@@ -404,7 +405,7 @@ int gen_KB(int M, int N) {
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
                         float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                        const admm_batch_reducer* red);
+                        const Traj& tr, const admm_batch_reducer* red);
 
 // the caller's cross-shard sum of an M x N map (isotropic prox over a sharded batch)
 int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStream_t s) {
@@ -447,8 +448,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     }
 
     if (generic_shape(M, N)) {
-        if (tr.s || tr.v) return fail(ADMM_E_UNSUPPORTED, "trajectory recording (adjoint) needs a power-of-two shape");
-        return run_forward_generic(ln, y, x_out, M, N, planes, kh, lambda, rho, iso, maxit, ws, lay, red);
+        return run_forward_generic(ln, y, x_out, M, N, planes, kh, lambda, rho, iso, maxit, ws, lay, tr, red);
     }
     if (fused_shape(M, N, iso != 0) && !tr.v && fused_enabled()) {
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
@@ -552,7 +552,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
                         float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                        const admm_batch_reducer* red) {
+                        const Traj& tr, const admm_batch_reducer* red) {
     namespace g = admm::gen;
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
@@ -597,9 +597,13 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         if (rc) return rc;
     }
     const int ng = iso_ngroups(planes);
+    const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
     for (int it = 1; it <= maxit; ++it) {
+        // trajectory for h_bar: the dim-2 spectrum of iteration it before the multiply
+        float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * planes * N * H : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 0, 1.0f);
+            hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB,
+                               vsave ? 4 : 0, 1.0f, vsave, (float*)nullptr);
         });
         if (rc) return rc;
         const bool last = it == maxit;
@@ -611,6 +615,10 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         if (!iso) {
             float* so = (it & 1) ? sbuf[1] : sbuf[0];   // iteration 1 reads nothing (first)
             float* sn = (it & 1) ? sbuf[0] : sbuf[1];
+            if (tr.s) {   // s_it into its own trajectory slot
+                so = it >= 2 ? tr.s + (size_t)(it - 2) * sstride : sbuf[0];
+                sn = tr.s + (size_t)(it - 1) * sstride;
+            }
             rc = ln.run(ADMM_K_LINE, [&] {
                 hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, tau,
                                    rho, it == 1 ? 1 : 0);
@@ -619,9 +627,15 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             continue;
         }
         float* sa = sbuf[0];
+        const float* s_in = sbuf[0];
+        if (tr.s) {
+            s_in = it >= 2 ? tr.s + (size_t)(it - 2) * sstride : sbuf[0];
+            sa = tr.s + (size_t)(it - 1) * sstride;
+        }
+        float* nrm_out = tr.nrm ? tr.nrm + (size_t)(it - 1) * MN : nullptr;
         rc = ln.run(ADMM_K_LINE, [&] {
-            hipLaunchKernelGGL(g::iso_a_kernel, dim3(N / T, ng), dim3(256), (size_t)T * M * 4, s, xg, sa, fmap, part, M,
-                               N, (int)planes, iso_group(planes), T, it == 1 ? 1 : 0);
+            hipLaunchKernelGGL(g::iso_a_kernel, dim3(N / T, ng), dim3(256), (size_t)T * M * 4, s, xg, s_in, sa, fmap,
+                               part, M, N, (int)planes, iso_group(planes), T, it == 1 ? 1 : 0);
         });
         if (rc) return rc;
         const int nb = (int)((MN + 63) / 64);   // 64 pixels per block (group_sum)
@@ -634,11 +648,11 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             rc = call_reducer(red, fmap, MN, s);
             if (rc) return rc;
             rc = ln.run(ADMM_K_NORM, [&] {
-                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, (float*)nullptr);
+                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, nrm_out);
             });
         } else {
             rc = ln.run(ADMM_K_NORM, [&] {
-                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, (float*)nullptr);
+                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, nrm_out);
             });
         }
         if (rc) return rc;
@@ -689,10 +703,12 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     };
     const size_t MN = (size_t)M * N;
     const int K = maxit < 1 ? 1 : maxit;
-    const int T = line_T(M, N);
+    const bool gen = generic_shape(M, N);
+    const int T = gen ? gen_T(M, N) : line_T(M, N);
     const bool hq = want_h && kh > 0;
     b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * 2 * MN * 4);
-    b.traj_v = hq ? take((size_t)K * planes * MN * 4) : 0;
+    // forward dim-2 spectra per iteration: packed M/2 x N (power of two) or M/2+1 x N bins (generic)
+    b.traj_v = hq ? take((size_t)K * planes * (gen ? (size_t)(M / 2 + 1) * N * 8 : MN * 4)) : 0;
     b.sig = hq ? take((size_t)(M / 2 + 1) * N * 16) : 0;
     b.sbA = take(planes * 2 * MN * 4);
     b.sbB = take(planes * 2 * MN * 4);
@@ -712,7 +728,12 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     b.rpart = take((size_t)K * b.nblk_line * 2 * 8);
     b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 4) : 0;
     b.Q = hq ? take((size_t)(M / 2 + 1) * N * 8) : 0;
-    b.TY = N < 8 ? N : 8;
+    b.TY = 1;   // h_bar correlation tile: the largest of 8, 4, 2, 1 lines dividing N
+    for (int t = 8; t > 1; t >>= 1)
+        if (N % t == 0) {
+            b.TY = t;
+            break;
+        }
     b.nblk_corr = (int)(planes * (N / b.TY));
     b.hpart = kh > 0 ? take((size_t)b.nblk_corr * kh * kw * 8) : 0;
     b.hcorr = kh > 0 ? take((size_t)kh * kw * 8) : 0;
@@ -834,9 +855,6 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
-    if (generic_shape(M, N))
-        return fail(ADMM_E_UNSUPPORTED, "the adjoint needs a power-of-two shape (4<=M<=1024, 2<=N<=1024; got M=%d N=%d)",
-                    M, N);
     *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
     return ADMM_OK;
 }
@@ -866,9 +884,6 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
-    if (generic_shape(M, N))
-        return fail(ADMM_E_UNSUPPORTED, "the adjoint needs a power-of-two shape (4<=M<=1024, 2<=N<=1024; got M=%d N=%d)",
-                    M, N);
     const bool want_h = (phases == 1 ? want_hbar_rec != 0 : h_bar != nullptr) && kh > 0;
     // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
     const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
@@ -880,8 +895,9 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     Launcher ln{s, g_prof.on, {}};
     const size_t MN = (size_t)M * N;
     const int L = M / 2;
-    const int T = line_T(M, N);
-    const int KB = column_KB(M, N);
+    const bool gen = generic_shape(M, N);   // runtime-length path (admm_generic.hip, admm_generic_bwd.hip)
+    const int T = gen ? gen_T(M, N) : line_T(M, N);
+    const int KB = gen ? gen_KB(M, N) : column_KB(M, N);
     const float tau = lambda / rho;
     const int K = maxit;
     if (!x_out || (reinterpret_cast<uintptr_t>(x_out) & 15))
@@ -954,11 +970,73 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
     if (iso) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
     if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
-    if (!fused_adj) {
+    if (gen) {
+        // ---- runtime-length reverse sweep (admm_generic_bwd.hip): column, line inverse -> vbar_k in
+        // HBM, then the line adjoint (aniso) or ISO_ADJ_A -> ISO_ADJ_R -> ISO_ADJ_B ----
+        namespace g = admm::gen;
+        const int H = M / 2 + 1;
+        const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
+        const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
+        const size_t lfw = (size_t)2 * T * M * 8, lup = lfw + (size_t)(2 * T + 1) * M * 4;
+        const size_t lcol = (size_t)2 * KB * N * 8;
+        set_lds(g::line_fwd_kernel, lfw);
+        set_lds(g::line_inv_kernel, lfw);
+        set_lds(g::line_adj_kernel, lup);
+        set_lds(g::iso_adj_b_kernel, lup);
+        set_lds(g::column_kernel, lcol);
+        float* vb = reinterpret_cast<float*>(ws + bl.f.xg);
+        rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, ggl, dim3(256), lfw, s, x_bar, specA, twM, pM, N, T); });
+        if (rc) return rc;
+        for (int k = K; k >= 1; --k) {
+            float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * H : nullptr;
+            rc = ln.run(ADMM_K_COLUMN, [&] {
+                hipLaunchKernelGGL(g::column_kernel, ggc, dim3(256), lcol, s, specA, specB, Ct, Gt, twN, pN, H, KB,
+                                   want_h ? 8 : 0, 1.0f, vs, Qp);
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_LINE, [&] { hipLaunchKernelGGL(g::line_inv_kernel, ggl, dim3(256), lfw, s, specB, vb, twM, pM, N, T); });
+            if (rc) return rc;
+            const float* sk1 = k >= 2 ? tr.s + (size_t)(k - 2) * sstride : nullptr;
+            const float* skk = k < K ? tr.s + (size_t)(k - 1) * sstride : nullptr;
+            const float* sbi = k < K ? sb[k & 1] : nullptr;
+            float* sbo = sb[(k & 1) ^ 1];
+            double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
+            if (!iso) {
+                rc = ln.run(ADMM_K_ADJ, [&] {
+                    hipLaunchKernelGGL(g::line_adj_kernel, ggl, dim3(256), lup, s, vb, sk1, skk, xK, sbi, sbo, vsum, specA,
+                                       rp, twM, pM, N, T, tau, rho);
+                });
+                if (rc) return rc;
+                continue;
+            }
+            const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
+            rc = ln.run(ADMM_K_ADJ, [&] {
+                hipLaunchKernelGGL(g::iso_adj_a_kernel, dim3(N / T, (unsigned)ngi), dim3(256), (size_t)T * M * 4, s, vb,
+                                   sk1, skk, xK, nrm1, sbi, wbar, vsum, Rpart, rp, M, N, (int)planes, iso_group(planes),
+                                   T, tau, rho);
+            });
+            if (rc) return rc;
+            if (k == 1) break;
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_adj_r_kernel, dim3(kIsoAdjRBlocks), dim3(kThreads), 0, s, Rpart, Rmap,
+                                   nrm1, ngi, MN, tau, rp + (size_t)bl.nblk_isoA * 2);
+            });
+            if (rc) return rc;
+            if (red) {
+                rc = call_reducer(red, Rmap, MN, s);
+                if (rc) return rc;
+            }
+            rc = ln.run(ADMM_K_ADJ, [&] {
+                hipLaunchKernelGGL(g::iso_adj_b_kernel, ggl, dim3(256), lup, s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA,
+                                   twM, pM, N, T, tau);
+            });
+            if (rc) return rc;
+        }
+    } else if (!fused_adj) {
         rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
         if (rc) return rc;
     }
-    for (int k = fused_adj ? 0 : K; k >= 1; --k) {
+    for (int k = (fused_adj || gen) ? 0 : K; k >= 1; --k) {
         float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
             launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
@@ -1012,12 +1090,29 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     double* hA = want_h ? reinterpret_cast<double*>(ws + bl.hA) : nullptr;
     if (kh > 0) {
         // y_bar = H vsum  (centred circular convolution, spectrally)
-        rc = ln.run(ADMM_K_FINAL, [&] { launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
-        if (rc) return rc;
-        rc = ln.run(ADMM_K_FINAL, [&] { launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
-        if (rc) return rc;
-        rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, specB, y_bar, twM, N); });
-        if (rc) return rc;
+        if (gen) {
+            namespace g = admm::gen;
+            const int H = M / 2 + 1;
+            const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
+            const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
+            const size_t lfw = (size_t)2 * T * M * 8, lcol = (size_t)2 * KB * N * 8;
+            rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, ggl, dim3(256), lfw, s, vsum, specA, twM, pM, N, T); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(g::column_kernel, ggc, dim3(256), lcol, s, specA, specB, Ct, Gt, twN, pN, H, KB, 2, 1.0f,
+                                   (float2*)nullptr, (float*)nullptr);
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_inv_kernel, ggl, dim3(256), lfw, s, specB, y_bar, twM, pM, N, T); });
+            if (rc) return rc;
+        } else {
+            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] { launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, specB, y_bar, twM, N); });
+            if (rc) return rc;
+        }
         if (h_bar) {
             double* hpart = reinterpret_cast<double*>(ws + bl.hpart);
             rc = ln.run(ADMM_K_FINAL, [&] {

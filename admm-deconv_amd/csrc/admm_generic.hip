@@ -177,11 +177,15 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
 }
 
 // dim-2 transforms of KB spectral columns: FFT_N, x multiplier, IFFT_N (grid (ceil(H / KB), planes)).
-//   mode 0: x cs * Ct (x-update C / (MN), ops.jl:86);  mode 1: x Gt (H^T: conj(Sigma_c) / (MN))
+//   mode & 3 = 0: x cs * Ct (x-update C / (MN), ops.jl:86 -- and its adjoint A^-1);
+//              1: x Gt (H^T: conj(Sigma_c) / (MN));  2: x conj(Gt) (H, y_bar = H Vsum in the adjoint)
+//   mode & 4: store the dim-2 spectrum before the multiply to vsave [plane][kj][k] (trajectory, h_bar)
+//   mode & 8: Qp[plane][kj][k] += Re(conj(G) V) against vsave (adjoint, h_bar)
 __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
                                                      const float2* __restrict__ twN, FPlan pN, int H, int KB,
-                                                     int mode, float cs) {
+                                                     int mode, float cs, float2* __restrict__ vsave = nullptr,
+                                                     float* __restrict__ Qp = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int N = pN.n;
     float2* A = reinterpret_cast<float2*>(smem_raw);
@@ -202,7 +206,14 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
         if (c >= kc) continue;
         const size_t q = (size_t)kj * H + k0 + c;
         const float2 v = R[c * N + kj];
-        R[c * N + kj] = mode == 0 ? cscale(v, cs * Ct[q]) : cmul(v, Gt[q]);
+        const size_t pq = (size_t)plane * N * H + q;
+        if (mode & 4) vsave[pq] = v;
+        if (mode & 8) {
+            const float2 fv = vsave[pq];
+            Qp[pq] += v.x * fv.x + v.y * fv.y;
+        }
+        const int mul = mode & 3;
+        R[c * N + kj] = mul == 0 ? cscale(v, cs * Ct[q]) : cmul(v, mul == 1 ? Gt[q] : cconj(Gt[q]));
     }
     __syncthreads();
     const float2* Z = fft<true>(R, O, KB, N, pN, twN);
@@ -259,11 +270,12 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     }
 }
 
-// isotropic step A (grid (N / T, plane groups)): s = D x + (1 - f_old) s_old written in place, and the
+// isotropic step A (grid (N / T, plane groups)): s = D x + (1 - f_old) s_old (s_in -> s, in place unless
+// a trajectory is recorded), and the
 // group's partial sum of s^2 over planes and both channels per pixel (ops.jl:6)
-__global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x, float* s, const float* __restrict__ fmap,
-                                                    float* __restrict__ part, int M, int N, int planes, int G, int T,
-                                                    int first) {
+__global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x, const float* s_in, float* s,
+                                                    const float* __restrict__ fmap, float* __restrict__ part, int M,
+                                                    int N, int planes, int G, int T, int first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float* acc = reinterpret_cast<float*>(smem_raw);
     const size_t MN = (size_t)M * N;
@@ -273,13 +285,14 @@ __global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x,
     for (int plane = grp * G; plane < p_end; ++plane) {
         const float* xp = x + (size_t)plane * MN;
         float* sp = s + (size_t)plane * 2 * MN;
+        const float* si = s_in + (size_t)plane * 2 * MN;   // s_in may alias s (same element read first)
         for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
             const int t = idx / M, i = idx - t * M;
             const int jj = j0 + t, jp = wrap(jj - 1, N);
             const size_t o = (size_t)jj * M + i;
             const float f = first ? 0.0f : fmap[o];
             const float xc = xp[o];
-            const float a0 = first ? 0.0f : sp[o], a1 = first ? 0.0f : sp[MN + o];
+            const float a0 = first ? 0.0f : si[o], a1 = first ? 0.0f : si[MN + o];
             const float s0 = (xc - xp[(size_t)jp * M + i]) + (a0 - f * a0);
             const float s1 = (xc - xp[(size_t)jj * M + wrap(i - 1, M)]) + (a1 - f * a1);
             sp[o] = s0;

@@ -22,8 +22,8 @@
  *    thread-local message for the last failing call.
  *  - Supported shapes: any 2 <= M, N <= 4096 with kh <= M, kw <= N (the reference accepts any
  *    M x N >= 2 x 2 through FFTW/CUFFT).  Powers of two with 4 <= M <= 1024, 2 <= N <= 1024 run
- *    the tuned kernels; every other shape runs a runtime-length mixed-radix path (forward only:
- *    the adjoint returns ADMM_E_UNSUPPORTED for those shapes). 
+ *    the tuned kernels; every other shape runs a runtime-length mixed-radix path (forward and
+ *    adjoint).
  */
 #ifndef ADMM_DECONV_H
 #define ADMM_DECONV_H

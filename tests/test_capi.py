@@ -78,10 +78,14 @@ def test_product_path_has_no_cpu_fallback():
 
 
 @pytest.mark.parametrize("M,N", [(48, 64), (100, 75), (37, 29), (64, 2048)])
-def test_generic_shapes_forward_only(M, N):
-    """Shapes outside the power-of-two kernels run the generic path (forward); the adjoint refuses them."""
+def test_generic_shapes_workspace(M, N):
+    """Shapes outside the power-of-two kernels run the runtime-length path, forward and adjoint."""
     out = ctypes.c_size_t(0)
     L = _lib.load()
     assert L.admm_tvd_workspace_bytes(M, N, 1, 2, 5, 5, 0, ctypes.byref(out)) == _lib.ADMM_OK
     assert out.value >= 2 * M * N * 4 * 4
-    assert L.admm_tvd_backward_workspace_bytes(M, N, 1, 2, 5, 5, 0, 4, 0, ctypes.byref(out)) == _lib.ADMM_E_UNSUPPORTED
+    for iso in (0, 1):
+        for want_h in (0, 1):
+            assert L.admm_tvd_backward_workspace_bytes(M, N, 1, 2, 5, 5, iso, 4, want_h, ctypes.byref(out)) == _lib.ADMM_OK
+            # trajectory (3 slots of s) + the dim-2 spectra when h_bar is wanted
+            assert out.value >= 3 * 2 * 2 * M * N * 4 + want_h * 4 * 2 * (M // 2 + 1) * N * 8
