@@ -392,16 +392,31 @@ admm::gen::FPlan make_fplan(int n) {
     return p;
 }
 // lines per block: the largest of 8, 4, 2, 1 dividing N with T * M <= 4096 (LDS ~ 24 T M bytes)
+// experiment knobs: ADMM_GEN_TM (max T x M of a line block), ADMM_GEN_KN (max KB x N of a column block)
+int gen_env(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v >= 256 && v <= 8192 ? v : dflt;
+}
 int gen_T(int M, int N) {
+    // 2048: smaller blocks, more of them resident per CU (480x640: 1.3x over 4096, tools/gen_knobs.sh)
+    const int tm = gen_env("ADMM_GEN_TM", 2048);
     for (int t = 8; t > 1; t >>= 1)
-        if (N % t == 0 && t * M <= 4096) return t;
+        if (N % t == 0 && t * M <= tm) return t;
     return 1;
 }
 int gen_KB(int M, int N) {
-    int kb = 4096 / N;
+    int kb = gen_env("ADMM_GEN_KN", 2048) / N;
     kb = kb < 1 ? 1 : (kb > 16 ? 16 : kb);
     return kb > M / 2 + 1 ? M / 2 + 1 : kb;
 }
+// dynamic LDS of the runtime-length kernels: ping-pong FFT buffers (+ the two D^T channels of the
+// update kernels) + the twiddle table staged by gen::stage_tw (8 n bytes, 8-B aligned)
+size_t gen_lds_line(int M, int T, bool upd) {
+    const size_t base = (size_t)2 * T * M * 8 + (upd ? (size_t)(2 * T + 1) * M * 4 : 0);
+    return ((base + 7) & ~size_t(7)) + (size_t)M * 8;
+}
+size_t gen_lds_col(int N, int KB) { return (size_t)2 * KB * N * 8 + (size_t)N * 8; }
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
                         float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
@@ -573,9 +588,9 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
     const int T = gen_T(M, N), KB = gen_KB(M, N);
     const dim3 gl(N / T, (unsigned)planes), gc((H + KB - 1) / KB, (unsigned)planes);
-    const size_t lfw = (size_t)2 * T * M * 8;                        // line_fwd / line_inv
-    const size_t lup = lfw + (size_t)(2 * T + 1) * M * 4;            // line_upd / iso_b
-    const size_t lcol = (size_t)2 * KB * N * 8;
+    const size_t lfw = gen_lds_line(M, T, false);                    // line_fwd / line_inv
+    const size_t lup = gen_lds_line(M, T, true);                     // line_upd / iso_b
+    const size_t lcol = gen_lds_col(N, KB);
     set_lds(g::line_fwd_kernel, lfw);
     set_lds(g::line_inv_kernel, lfw);
     set_lds(g::line_upd_kernel, lup);
@@ -977,8 +992,8 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         const int H = M / 2 + 1;
         const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
         const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
-        const size_t lfw = (size_t)2 * T * M * 8, lup = lfw + (size_t)(2 * T + 1) * M * 4;
-        const size_t lcol = (size_t)2 * KB * N * 8;
+        const size_t lfw = gen_lds_line(M, T, false), lup = gen_lds_line(M, T, true);
+        const size_t lcol = gen_lds_col(N, KB);
         set_lds(g::line_fwd_kernel, lfw);
         set_lds(g::line_inv_kernel, lfw);
         set_lds(g::line_adj_kernel, lup);
@@ -1095,7 +1110,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             const int H = M / 2 + 1;
             const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
             const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
-            const size_t lfw = (size_t)2 * T * M * 8, lcol = (size_t)2 * KB * N * 8;
+            const size_t lfw = gen_lds_line(M, T, false), lcol = gen_lds_col(N, KB);
             rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, ggl, dim3(256), lfw, s, vsum, specA, twM, pM, N, T); });
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] {

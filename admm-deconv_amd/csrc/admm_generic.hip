@@ -135,6 +135,15 @@ __device__ float2* fft(float2* a, float2* b, int cnt, int stride, const FPlan& p
 }
 
 __device__ __forceinline__ int wrap(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+
+// The n twiddles copied to LDS at byte offset off of the dynamic LDS (8-B aligned; the host adds 8 n + 8
+// bytes): the butterflies read them once per twiddled point, from global memory that is an L1/L2 round
+// trip each.  Visible after the caller's next block barrier.
+__device__ __forceinline__ const float2* stage_tw(unsigned char* smem, size_t off, const float2* __restrict__ tw, int n) {
+    float2* d = reinterpret_cast<float2*>(smem + ((off + 7) & ~size_t(7)));
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = tw[i];
+    return d;
+}
 __device__ __forceinline__ float clip(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
 __device__ __forceinline__ float phi(float s, float tau) { return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s; }
 
@@ -147,9 +156,10 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
     float2* B = A + (size_t)T * M;
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* sp = src + ((size_t)plane * N + j0) * M;
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) A[idx] = make_float2(sp[idx], 0.0f);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
         const int t = idx / H, k = idx - t * H;
@@ -166,12 +176,13 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     float2* B = A + (size_t)T * M;
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = idx / M, k = idx - t * M;
         A[idx] = k < H ? sp[t * H + k] : cconj(sp[t * H + (M - k)]);
     }
     __syncthreads();
-    const float2* R = fft<true>(A, B, T, M, pM, twM);
+    const float2* R = fft<true>(A, B, T, M, pM, tw);
     float* dp = dst + ((size_t)plane * N + j0) * M;
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) dp[idx] = R[idx].x;
 }
@@ -194,12 +205,13 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
     const int kc = min(KB, H - k0);
     const float2* sp = src + (size_t)plane * N * H + k0;
     float2* dp = dst + (size_t)plane * N * H + k0;
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * KB * N, twN, N);
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
         const int j = idx / KB, c = idx - j * KB;
         A[c * N + j] = c < kc ? sp[(size_t)j * H + c] : make_float2(0.f, 0.f);
     }
     __syncthreads();
-    float2* R = fft<false>(A, B, KB, N, pN, twN);
+    float2* R = fft<false>(A, B, KB, N, pN, tw);
     float2* O = R == A ? B : A;
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
         const int kj = idx / KB, c = idx - kj * KB;
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
         R[c * N + kj] = mul == 0 ? cscale(v, cs * Ct[q]) : cmul(v, mul == 1 ? Gt[q] : cconj(Gt[q]));
     }
     __syncthreads();
-    const float2* Z = fft<true>(R, O, KB, N, pN, twN);
+    const float2* Z = fft<true>(R, O, KB, N, pN, tw);
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
         const int j = idx / KB, c = idx - j * KB;
         if (c < kc) dp[(size_t)j * H + c] = Z[c * N + j];
@@ -261,8 +273,9 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
     }
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
         const int t = idx / H, k = idx - t * H;
@@ -332,8 +345,9 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
     }
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
         const int t = idx / H, k = idx - t * H;

@@ -126,8 +126,9 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(g, 0.0f);
     }
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
         const int t = idx / H, k = idx - t * H;
@@ -230,8 +231,9 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(g, 0.0f);
     }
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, twM);
+    const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
         const int t = idx / H, k = idx - t * H;

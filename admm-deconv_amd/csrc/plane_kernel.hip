@@ -183,6 +183,10 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     float2 gf[MODE == 1 ? 32 : 1];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
+#ifdef PLANE_EXPT_NOCF
+        // timing experiment only (wrong results): no multiplier loads in the x-update column phase
+        if constexpr (MODE == 0) { cf[j] = 1.0f / 65536.0f; continue; }
+#endif
         if constexpr (MODE == 0) cf[j] = bld1(Cf, t * 4, (HALF * 32 + j) * kPT * 4);
         else gf[j] = bld2(Gf, t * 8, (HALF * 32 + j) * kPT * 8);
     }
