@@ -541,13 +541,18 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
                 break;
             }
         }
+        // iteration 1 has no s_0 to read (zero init, ops.jl:48-49): its loads go to a resource of size 0,
+        // which returns zeros without touching memory
         if constexpr (TRAJ) {
             float4* tb = traj + plane * 64 * kPT;
-            const rsrc_t sld = make_rsrc(tb + (size_t)(k >= 2 ? k - 2 : 0) * traj_slot, 64 * kPT * 16);
+            const rsrc_t sld = make_rsrc(tb + (size_t)(k >= 2 ? k - 2 : 0) * traj_slot, k >= 2 ? 64 * kPT * 16 : 0);
             const rsrc_t sst = make_rsrc(tb + (size_t)(k - 1) * traj_slot, 64 * kPT * 16);
             row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
         } else {
-            row_update<kStage>(S, sp, sp, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            // ... and s_{K-1} is never read (iteration K stops at x): its stores drop the same way
+            const rsrc_t sld = k >= 2 ? sp : make_rsrc(sln, 0);
+            const rsrc_t sst = k <= K - 2 ? sp : make_rsrc(sln, 0);
+            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
         }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
         line_forward_pair(S, hb);

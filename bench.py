@@ -46,9 +46,10 @@ def canonical_bytes(M, N, K):
 
 def plane_bytes_per_px(K):
     """Fused per-plane kernel (plane_kernel.hip), HBM bytes per pixel for one K-iteration solve:
-    y in (4) + H^T y out (4) + (K-1) x [H^T y in (4) + s out (8)] + (K-2) x s in (8) + x out (4).
+    y in (4) + H^T y out (4) + (K-1) x H^T y in (4) + (K-2) x [s out (8) + s in (8)] + x out (4)
+    (s_k is written for k = 1..K-2 and read by the next iteration; s_{K-1} is never read).
     The line spectrum never leaves the CU, so this is the algorithm's minimum."""
-    return 12 + 12 * (K - 1) + 8 * max(K - 2, 0)
+    return 12 + 4 * (K - 1) + 16 * max(K - 2, 0)
 
 
 def kernel_bytes_per_plane(M, N, K):
