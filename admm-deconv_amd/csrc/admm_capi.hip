@@ -155,6 +155,12 @@ int column_KB(int M, int N) {
     if (KB > 32) KB = 32;
     return KB;
 }
+// reverse sweep line tile: the isotropic adjoint kernels (ISO_ADJ_A / _B) run best with 4 lines per
+// block (c5 iso: 55.4 -> 51.9 ms of adjoint per step, tools/iso_knobs.sh); the rest keeps line_T
+int bwd_line_T(int M, int N, bool iso) {
+    const int t = line_T(M, N);
+    return iso && t > 4 ? 4 : t;
+}
 size_t column_lds(int N, int KB) { return (size_t)N * 16 + (size_t)KB * (N + 1) * 8; }
 size_t iso_a_lds(int M, int T) { return (size_t)M * 8 + 3 * (size_t)(T + 1) * (M / 2) * 8; }
 size_t iso_b_lds(int M, int T) { return (size_t)M * 8 + (size_t)(2 * T + 1) * M * 4 + 2 * (size_t)T * (M / 2) * 8; }
@@ -719,7 +725,7 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     const size_t MN = (size_t)M * N;
     const int K = maxit < 1 ? 1 : maxit;
     const bool gen = generic_shape(M, N);
-    const int T = gen ? gen_T(M, N) : line_T(M, N);
+    const int T = gen ? gen_T(M, N) : bwd_line_T(M, N, iso);
     const bool hq = want_h && kh > 0;
     b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * 2 * MN * 4);
     // forward dim-2 spectra per iteration: packed M/2 x N (power of two) or M/2+1 x N bins (generic)
@@ -911,7 +917,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     const size_t MN = (size_t)M * N;
     const int L = M / 2;
     const bool gen = generic_shape(M, N);   // runtime-length path (admm_generic.hip, admm_generic_bwd.hip)
-    const int T = gen ? gen_T(M, N) : line_T(M, N);
+    const int T = gen ? gen_T(M, N) : bwd_line_T(M, N, iso != 0);
     const int KB = gen ? gen_KB(M, N) : column_KB(M, N);
     const float tau = lambda / rho;
     const int K = maxit;
