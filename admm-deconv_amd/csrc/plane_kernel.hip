@@ -293,7 +293,10 @@ template <bool STAGED = false>
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sps, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho) {
-    constexpr int CH = 2;            // registers per chunk
+#ifndef PLANE_CH
+#define PLANE_CH 2
+#endif
+    constexpr int CH = PLANE_CH;     // registers per chunk
 #ifndef PLANE_PD
 #define PLANE_PD 1
 #endif
