@@ -397,7 +397,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                                                              const float* __restrict__ sk1, const float* __restrict__ sk,
                                                              const float* __restrict__ xK,
                                                              const float* __restrict__ nrm1, const float* __restrict__ nrm0,
-                                                             const float* __restrict__ sb_in, float* __restrict__ wbar,
+                                                             const float* __restrict__ sb_in, float* __restrict__ vbar_out,
                                                              float* __restrict__ vsum, float* __restrict__ rpartial,
                                                              double* __restrict__ part, const float2* __restrict__ twM,
                                                              int N, int planes, int G, float tau, float rho,
@@ -504,6 +504,9 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
             acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
             *vs = acc;
             if (!first_k) {
+                // vbar_k for ISO_ADJ_B, which forms wbar = rho D vbar itself (4 B/px here and ~5 there,
+                // against 8 + 8 for a stored two-channel wbar)
+                *reinterpret_cast<float4*>(vbar_out + (size_t)plane * MN + off) = vc;
                 float b0[4] = {0, 0, 0, 0}, b1[4] = {0, 0, 0, 0};   // sbar_k
                 if (sb_in) {
                     const float4 a = *reinterpret_cast<const float4*>(sb_in + poff + off);
@@ -520,8 +523,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                     rho_acc += ph * (a0[q] * dv0[q] + a1[q] * dv1[q]);
                     rr[q] = a0[q] * (2.0f * w0[q] - b0[q]) + a1[q] * (2.0f * w1[q] - b1[q]);
                 }
-                *reinterpret_cast<float4*>(wbar + poff + off) = make_float4(w0[0], w0[1], w0[2], w0[3]);
-                *reinterpret_cast<float4*>(wbar + poff + MN + off) = make_float4(w1[0], w1[1], w1[2], w1[3]);
+
                 racc[it].x += rr[0]; racc[it].y += rr[1]; racc[it].z += rr[2]; racc[it].w += rr[3];
             }
         }
@@ -562,11 +564,11 @@ __global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __rest
 
 // sbar_{k-1} = (2f - 1) wbar + (1 - f) sbar_k + [Nrm > tau] (tau/Nrm^3) R s_{k-1}; g = D^T sbar -> rFFT
 template <int L, int T>
-__global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __restrict__ wbar, const float* __restrict__ sb_in,
+__global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __restrict__ vbar, const float* __restrict__ sb_in,
                                                              const float* __restrict__ sk1, const float* __restrict__ nrm1,
                                                              const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                              float2* __restrict__ spec0, const float2* __restrict__ twM,
-                                                             int N, float tau) {
+                                                             int N, float tau, float rho) {
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;
@@ -600,9 +602,16 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
             cs[q] = 1.0f - f;
             cf[q] = n4[q] > tau ? tau / (n4[q] * n4[q] * n4[q]) * r4[q] : 0.0f;
         }
+        // wbar = rho D vbar_k, bitwise as ISO_ADJ_A formed it
+        const float* vp = vbar + (size_t)plane * MN;
+        const float4 vc = *reinterpret_cast<const float4*>(vp + off);
+        const float4 vu = *reinterpret_cast<const float4*>(vp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
+        const float vl = vp[(size_t)((j0 + t) & (N - 1)) * M + ((i - 1) & (M - 1))];
+        const float4 wb0 = make_float4(rho * (vc.x - vu.x), rho * (vc.y - vu.y), rho * (vc.z - vu.z), rho * (vc.w - vu.w));
+        const float4 wb1 = make_float4(rho * (vc.x - vl), rho * (vc.y - vc.x), rho * (vc.z - vc.y), rho * (vc.w - vc.z));
         for (int ch = 0; ch < (t < T ? 2 : 1); ++ch) {
             const size_t o = poff + (size_t)ch * MN + off;
-            const float4 w = *reinterpret_cast<const float4*>(wbar + o);
+            const float4 w = ch == 0 ? wb0 : wb1;
             const float4 a = *reinterpret_cast<const float4*>(sk1 + o);
             float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
             if (sb_in) b = *reinterpret_cast<const float4*>(sb_in + o);

@@ -737,7 +737,7 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     if (iso) {
         const size_t ng = iso_ngroups(planes);
         b.traj_n = take((size_t)(K > 1 ? K - 1 : 1) * MN * 4);
-        b.wbar = take(planes * 2 * MN * 4);
+        b.wbar = take(planes * MN * 4);   // vbar_k handed from ISO_ADJ_A to ISO_ADJ_B
         b.Rmap = take(MN * 4);
         b.Rpart = take(ng * MN * 4);
         b.nblk_isoA = (int)(ng * (N / T));
@@ -825,12 +825,12 @@ int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const floa
 
 int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* wbar, const float* sb_in,
                      const float* sk1, const float* nrm1, const float* Rmap, float* sb_out, float2* spec0,
-                     const float2* twM, int N, float tau) {
+                     const float2* twM, int N, float tau, float rho) {
 #define X(l, t)                                                                                                 \
     if (L == l && T == t) {                                                                                     \
         set_lds(iso_adj_b_kernel<l, t>, lds);                                                                   \
         iso_adj_b_kernel<l, t><<<g, kThreads, lds, s>>>(wbar, sb_in, sk1, nrm1, Rmap, sb_out, spec0, twM, N,    \
-                                                         tau);                                                  \
+                                                         tau, rho);                                             \
         return 0;                                                                                               \
     }
     ADMM_LT_CASES(X)
@@ -1049,7 +1049,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             }
             rc = ln.run(ADMM_K_ADJ, [&] {
                 hipLaunchKernelGGL(g::iso_adj_b_kernel, ggl, dim3(256), lup, s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA,
-                                   twM, pM, N, T, tau);
+                                   twM, pM, N, T, tau, rho);
             });
             if (rc) return rc;
         }
@@ -1097,7 +1097,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             if (rc) return rc;
         }
         rc = ln.run(ADMM_K_ADJ, [&] {
-            launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau);
+            launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau, rho);
         });
         if (rc) return rc;
     }

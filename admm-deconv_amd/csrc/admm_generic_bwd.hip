@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict__ vb, const float* __restrict__ sk1,
                                                         const float* __restrict__ sk, const float* __restrict__ xK,
                                                         const float* __restrict__ nrm1, const float* __restrict__ sb_in,
-                                                        float* __restrict__ wbar, float* __restrict__ vsum,
+                                                        float* __restrict__ vbar_out, float* __restrict__ vsum,
                                                         float* __restrict__ rpartial, double* __restrict__ part,
                                                         int M, int N, int planes, int G, int T, float tau, float rho) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -182,8 +182,7 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
                 const float w0 = rho * dv0, w1 = rho * dv1;
                 racc += (2.0f * f - 1.0f) * (a0 * dv0 + a1 * dv1);   // phi(s) = (2f - 1) s
                 acc[idx] += a0 * (2.0f * w0 - b0) + a1 * (2.0f * w1 - b1);
-                wbar[poff + o] = w0;
-                wbar[poff + MN + o] = w1;
+                vbar_out[(size_t)plane * MN + o] = vc;   // GEN_ISO_ADJ_B forms wbar = rho D vbar itself
             }
         }
     }
@@ -196,11 +195,11 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
 
 // Iso reverse step B (grid (N / T, planes)): sbar_{k-1} = (2f - 1) wbar + (1 - f) sbar_k
 // + [Nrm > tau] (tau / Nrm^3) R s_{k-1};  D^T sbar_{k-1} -> dim-1 FFT
-__global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict__ wbar, const float* __restrict__ sb_in,
+__global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict__ vbar, const float* __restrict__ sb_in,
                                                         const float* __restrict__ sk1, const float* __restrict__ nrm1,
                                                         const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                         float2* __restrict__ spec, const float2* __restrict__ twM,
-                                                        FPlan pM, int N, int T, float tau) {
+                                                        FPlan pM, int N, int T, float tau, float rho) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
@@ -217,10 +216,14 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
         const float f = max0_nan(1.0f - tau / nn);
         const float cw = 2.0f * f - 1.0f, cs = 1.0f - f;
         const float cf = nn > tau ? tau / (nn * nn * nn) * Rmap[o] : 0.0f;
+        const float* vp = vbar + (size_t)plane * MN;
+        const int j = wrap(j0 + t, N);
+        const float vc = vp[o];
+        const float wb[2] = {rho * (vc - vp[(size_t)wrap(j - 1, N) * M + i]), rho * (vc - vp[(size_t)j * M + wrap(i - 1, M)])};
         for (int ch = 0; ch < (t < T ? 2 : 1); ++ch) {
             const size_t q = poff + (size_t)ch * MN + o;
             const float b = sb_in ? sb_in[q] : 0.0f;
-            const float r = cw * wbar[q] + cs * b + cf * sk1[q];
+            const float r = cw * wb[ch] + cs * b + cf * sk1[q];
             (ch == 0 ? W0 : W1)[idx] = r;
             if (t < T) sb_out[q] = r;
         }
