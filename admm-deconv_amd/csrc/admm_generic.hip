@@ -60,12 +60,23 @@ __device__ __forceinline__ void dft5(float2 (&x)[5]) {
     x[3] = csub(m2, e2);
 }
 
+// n / d for 0 <= n < 2^22, d >= 1 (exact): a v_rcp_f32 estimate is within 1 of the quotient there, and
+// one correction step fixes it -- a handful of VALU against ~30 for the compiler's integer-division
+// sequence (d is a runtime plan length, so there is no constant to divide by).  The reciprocal is loop
+// invariant at every call site.
+__device__ __forceinline__ int fdiv(int n, int d) {
+    const int q = (int)((float)n * __builtin_amdgcn_rcpf((float)d));
+    const int r = n - q * d;
+    return q + (r >= d) - (r < 0);
+}
+
 // one radix-R butterfly of a Stockham pass: src[j + a q] (a < R) twiddled by W_{Ns R}^{a k}, DFT_R,
 // to dst[(j / Ns) Ns R + k + c Ns]
 template <int R, bool INV>
 __device__ __forceinline__ void bfly(const float2* __restrict__ src, float2* __restrict__ dst, int j, int q, int Ns,
                                      int tstep, const float2* __restrict__ tw) {
-    const int k = j % Ns;
+    const int jn = fdiv(j, Ns);
+    const int k = j - jn * Ns;
     float2 v[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) {
@@ -79,7 +90,7 @@ __device__ __forceinline__ void bfly(const float2* __restrict__ src, float2* __r
     } else {
         dft<R, INV>(v);
     }
-    const int base = (j / Ns) * Ns * R + k;
+    const int base = jn * Ns * R + k;
 #pragma unroll
     for (int c = 0; c < R; ++c) dst[base + c * Ns] = v[c];
 }
@@ -88,8 +99,9 @@ __device__ __forceinline__ void bfly(const float2* __restrict__ src, float2* __r
 template <bool INV>
 __device__ __forceinline__ void bfly_any(const float2* __restrict__ src, float2* __restrict__ dst, int j, int q,
                                          int Ns, int R, int n, int tstep, const float2* __restrict__ tw) {
-    const int k = j % Ns;
-    const int base = (j / Ns) * Ns * R + k;
+    const int jn = fdiv(j, Ns);
+    const int k = j - jn * Ns;
+    const int base = jn * Ns * R + k;
     const int rstep = n / R;
     for (int c = 0; c < R; ++c) {
         float2 acc = make_float2(0.f, 0.f);
@@ -113,7 +125,7 @@ __device__ float2* fft(float2* a, float2* b, int cnt, int stride, const FPlan& p
         const int q = n / R;
         const int tstep = n / (Ns * R);
         for (int idx = threadIdx.x; idx < cnt * q; idx += blockDim.x) {
-            const int line = idx / q, j = idx - line * q;
+            const int line = fdiv(idx, q), j = idx - line * q;
             const float2* src = a + (size_t)line * stride;
             float2* dst = b + (size_t)line * stride;
             switch (R) {
@@ -162,7 +174,7 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
     const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = idx / H, k = idx - t * H;
+        const int t = fdiv(idx, H), k = idx - t * H;
         dp[idx] = R[t * M + k];
     }
 }
@@ -178,7 +190,7 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = idx / M, k = idx - t * M;
+        const int t = fdiv(idx, M), k = idx - t * M;
         A[idx] = k < H ? sp[t * H + k] : cconj(sp[t * H + (M - k)]);
     }
     __syncthreads();
@@ -207,14 +219,14 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
     float2* dp = dst + (size_t)plane * N * H + k0;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * KB * N, twN, N);
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
-        const int j = idx / KB, c = idx - j * KB;
+        const int j = fdiv(idx, KB), c = idx - j * KB;
         A[c * N + j] = c < kc ? sp[(size_t)j * H + c] : make_float2(0.f, 0.f);
     }
     __syncthreads();
     float2* R = fft<false>(A, B, KB, N, pN, tw);
     float2* O = R == A ? B : A;
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
-        const int kj = idx / KB, c = idx - kj * KB;
+        const int kj = fdiv(idx, KB), c = idx - kj * KB;
         if (c >= kc) continue;
         const size_t q = (size_t)kj * H + k0 + c;
         const float2 v = R[c * N + kj];
@@ -230,7 +242,7 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
     __syncthreads();
     const float2* Z = fft<true>(R, O, KB, N, pN, tw);
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
-        const int j = idx / KB, c = idx - j * KB;
+        const int j = fdiv(idx, KB), c = idx - j * KB;
         if (c < kc) dp[(size_t)j * H + c] = Z[c * N + j];
     }
 }
@@ -253,7 +265,7 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const int jj = wrap(j0 + t, N), jp = wrap(jj - 1, N);
         const size_t o = (size_t)jj * M + i;
         const float xc = xp[o];
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     __syncthreads();
     const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
     }
@@ -278,7 +290,7 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = idx / H, k = idx - t * H;
+        const int t = fdiv(idx, H), k = idx - t * H;
         dp[idx] = R[t * M + k];
     }
 }
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x,
         float* sp = s + (size_t)plane * 2 * MN;
         const float* si = s_in + (size_t)plane * 2 * MN;   // s_in may alias s (same element read first)
         for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-            const int t = idx / M, i = idx - t * M;
+            const int t = fdiv(idx, M), i = idx - t * M;
             const int jj = j0 + t, jp = wrap(jj - 1, N);
             const size_t o = (size_t)jj * M + i;
             const float f = first ? 0.0f : fmap[o];
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* sp = s + (size_t)plane * 2 * MN;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const size_t o = (size_t)wrap(j0 + t, N) * M + i;
         const float f = fmap[o];
         W0[idx] = f * sp[o] - (sp[o] - f * sp[o]);
@@ -341,7 +353,7 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     __syncthreads();
     const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
     }
@@ -350,7 +362,7 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = idx / H, k = idx - t * H;
+        const int t = fdiv(idx, H), k = idx - t * H;
         dp[idx] = R[t * M + k];
     }
 }

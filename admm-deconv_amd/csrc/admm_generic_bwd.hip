@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     const size_t poff = (size_t)plane * 2 * MN;
     const float* vp = vb + (size_t)plane * MN;
     for (int idx = threadIdx.x; idx < (T + 2) * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         V[idx] = vp[(size_t)wrap(j0 - 1 + t, N) * M + i];
     }
     __syncthreads();
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     const float* s1p = sk1 ? sk1 + poff : nullptr;
     float racc = 0.0f, tacc = 0.0f;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const int j = wrap(j0 + t, N);
         const size_t o = (size_t)j * M + i;
         const bool own = t < T;
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     if (!s1p) return;
     __syncthreads();   // W0/W1 complete; V (aliasing A, B) is dead
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(g, 0.0f);
     }
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = idx / H, k = idx - t * H;
+        const int t = fdiv(idx, H), k = idx - t * H;
         dp[idx] = R[t * M + k];
     }
 }
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
         const float* vp = vb + (size_t)plane * MN;
         const size_t poff = (size_t)plane * 2 * MN;
         for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-            const int t = idx / M, i = idx - t * M;
+            const int t = fdiv(idx, M), i = idx - t * M;
             const int j = j0 + t;
             const size_t o = (size_t)j * M + i;
             const float vc = vp[o];
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const size_t poff = (size_t)plane * 2 * MN;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const size_t o = (size_t)wrap(j0 + t, N) * M + i;
         const float nn = nrm1[o];
         const float f = max0_nan(1.0f - tau / nn);
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = idx / M, i = idx - t * M;
+        const int t = fdiv(idx, M), i = idx - t * M;
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         A[idx] = make_float2(g, 0.0f);
     }
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     const float2* R = fft<false>(A, B, T, M, pM, tw);
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = idx / H, k = idx - t * H;
+        const int t = fdiv(idx, H), k = idx - t * H;
         dp[idx] = R[t * M + k];
     }
 }
