@@ -156,6 +156,29 @@ __device__ __forceinline__ const float2* stage_tw(unsigned char* smem, size_t of
     for (int i = threadIdx.x; i < n; i += blockDim.x) d[i] = tw[i];
     return d;
 }
+// Real lines two per complex transform: lines 2p and 2p+1 are the real and imaginary parts of
+// transform p (P = ceil(T / 2) transforms instead of T, half the FFT work of a zero-imaginary line).
+// pack_real writes value v of line t, pixel i; with T odd, pad_odd zeroes the last transform's
+// imaginary part.  store_real_spectra separates the half spectra: X_2p = (Z + conj Z(-k)) / 2,
+// X_2p+1 = (Z - conj Z(-k)) / (2i), bins 0..M/2.
+__device__ __forceinline__ void pack_real(float2* A, int t, int i, int M, float v) {
+    reinterpret_cast<float*>(A)[2 * ((size_t)(t >> 1) * M + i) + (t & 1)] = v;
+}
+__device__ __forceinline__ void pad_odd(float2* A, int T, int M) {
+    if (T & 1)
+        for (int i = threadIdx.x; i < M; i += blockDim.x) A[(size_t)(T >> 1) * M + i].y = 0.0f;
+}
+__device__ __forceinline__ void store_real_spectra(const float2* __restrict__ R, float2* __restrict__ dp, int T, int M) {
+    const int H = M / 2 + 1;
+    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
+        const int t = fdiv(idx, H), k = idx - t * H;
+        const float2* Z = R + (size_t)(t >> 1) * M;
+        const float2 z = Z[k], zm = cconj(Z[k == 0 ? 0 : M - k]);
+        dp[idx] = (t & 1) ? make_float2(0.5f * (z.y - zm.y), -0.5f * (z.x - zm.x))
+                          : make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y + zm.y));
+    }
+}
+
 __device__ __forceinline__ float clip(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
 __device__ __forceinline__ float phi(float s, float tau) { return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s; }
 
@@ -169,14 +192,14 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* sp = src + ((size_t)plane * N + j0) * M;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) A[idx] = make_float2(sp[idx], 0.0f);
-    __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, tw);
-    float2* dp = spec + ((size_t)plane * N + j0) * H;
-    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = fdiv(idx, H), k = idx - t * H;
-        dp[idx] = R[t * M + k];
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        const int t = fdiv(idx, M);
+        pack_real(A, t, idx - t * M, M, sp[idx]);
     }
+    pad_odd(A, T, M);
+    __syncthreads();
+    const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
+    store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
 }
 
 // half spectra -> real lines (Hermitian extension, complex inverse, real part; unnormalised)
@@ -189,14 +212,26 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
-        const int t = fdiv(idx, M), k = idx - t * M;
-        A[idx] = k < H ? sp[t * H + k] : cconj(sp[t * H + (M - k)]);
+    // two lines per transform: Z = X_2p + i X_2p+1 (Hermitian extensions, DC / Nyquist bins taken real,
+    // which is what the real part of one line's inverse keeps) -> z = x_2p + i x_2p+1
+    const int P = (T + 1) / 2;
+    for (int idx = threadIdx.x; idx < P * M; idx += blockDim.x) {
+        const int p = fdiv(idx, M), k = idx - p * M;
+        const float2* sa = sp + (size_t)(2 * p) * H;
+        float2 xa = k < H ? sa[k] : cconj(sa[M - k]);
+        float2 xb = make_float2(0.0f, 0.0f);
+        if (2 * p + 1 < T) xb = k < H ? sa[H + k] : cconj(sa[H + M - k]);
+        if (k == 0 || 2 * k == M) xa.y = xb.y = 0.0f;
+        A[idx] = make_float2(xa.x - xb.y, xa.y + xb.x);
     }
     __syncthreads();
-    const float2* R = fft<true>(A, B, T, M, pM, tw);
+    const float2* R = fft<true>(A, B, P, M, pM, tw);
     float* dp = dst + ((size_t)plane * N + j0) * M;
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) dp[idx] = R[idx].x;
+    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        const int t = fdiv(idx, M);
+        const float2 v = R[(size_t)(t >> 1) * M + idx - t * M];
+        dp[idx] = (t & 1) ? v.y : v.x;
+    }
 }
 
 // dim-2 transforms of KB spectral columns: FFT_N, x multiplier, IFFT_N (grid (ceil(H / KB), planes)).
@@ -283,16 +318,13 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
+        pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
     }
+    pad_odd(A, T, M);
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, tw);
-    float2* dp = spec + ((size_t)plane * N + j0) * H;
-    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = fdiv(idx, H), k = idx - t * H;
-        dp[idx] = R[t * M + k];
-    }
+    const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
+    store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
 }
 
 // isotropic step A (grid (N / T, plane groups)): s = D x + (1 - f_old) s_old (s_in -> s, in place unless
@@ -355,16 +387,13 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        A[idx] = make_float2(fmaf(rho, dtw, hp[idx]), 0.0f);
+        pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
     }
+    pad_odd(A, T, M);
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, tw);
-    float2* dp = spec + ((size_t)plane * N + j0) * H;
-    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = fdiv(idx, H), k = idx - t * H;
-        dp[idx] = R[t * M + k];
-    }
+    const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
+    store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
 }
 
 }  // namespace gen

@@ -124,16 +124,13 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        A[idx] = make_float2(g, 0.0f);
+        pack_real(A, t, i, M, g);
     }
+    pad_odd(A, T, M);
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, tw);
-    float2* dp = spec + ((size_t)plane * N + j0) * H;
-    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = fdiv(idx, H), k = idx - t * H;
-        dp[idx] = R[t * M + k];
-    }
+    const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
+    store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
 }
 
 // Iso reverse step A (grid (N / T, plane groups)): per plane of the group D vbar, rho_bar partial,
@@ -232,16 +229,13 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float g = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        A[idx] = make_float2(g, 0.0f);
+        pack_real(A, t, i, M, g);
     }
+    pad_odd(A, T, M);
     const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
-    const float2* R = fft<false>(A, B, T, M, pM, tw);
-    float2* dp = spec + ((size_t)plane * N + j0) * H;
-    for (int idx = threadIdx.x; idx < T * H; idx += blockDim.x) {
-        const int t = fdiv(idx, H), k = idx - t * H;
-        dp[idx] = R[t * M + k];
-    }
+    const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
+    store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
 }
 
 }  // namespace gen
