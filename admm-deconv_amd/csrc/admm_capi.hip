@@ -419,7 +419,8 @@ int gen_KB(int M, int N) {
 // dynamic LDS of the runtime-length kernels: ping-pong FFT buffers (+ the two D^T channels of the
 // update kernels) + the twiddle table staged by gen::stage_tw (8 n bytes, 8-B aligned)
 size_t gen_lds_line(int M, int T, bool upd) {
-    const size_t base = (size_t)2 * T * M * 8 + (upd ? (size_t)(2 * T + 1) * M * 4 : 0);
+    // A, B hold ceil(T / 2) paired complex transforms (gen::pack_real: two real lines per transform)
+    const size_t base = (size_t)2 * ((T + 1) / 2) * M * 8 + (upd ? (size_t)(2 * T + 1) * M * 4 : 0);
     return ((base + 7) & ~size_t(7)) + (size_t)M * 8;
 }
 size_t gen_lds_col(int N, int KB) { return (size_t)2 * KB * N * 8 + (size_t)N * 8; }

@@ -6,8 +6,8 @@
 // RUNTIME lengths:
 //   * mixed-radix Stockham FFTs staged in LDS, radix 8/4/2/3/5 butterflies in registers and a direct
 //     DFT for any other prime factor (so every length works; 2-3-5-smooth lengths are the fast case);
-//   * dim-1 (contiguous, real) transforms as full complex FFTs of the real line, keeping bins
-//     0..M/2 (the rfft half spectrum, ops.jl:86) -- M may be odd;
+//   * dim-1 (contiguous, real) transforms as complex FFTs of two real lines at once (real and
+//     imaginary part), keeping bins 0..M/2 of each (the rfft half spectrum, ops.jl:86) -- M may be odd;
 //   * per iteration: GEN_COLUMN (dim-2 FFT, x C/(MN), inverse) -> GEN_LINE_INV (x to HBM) ->
 //     GEN_LINE_UPD (D, prox, dual, D^T, + H^T y, dim-1 FFT) -- or the iso triple GEN_ISO_A -> ISO_R ->
 //     GEN_ISO_B.  x takes one extra HBM round trip compared with the fused line kernel (8 B/px).
@@ -188,10 +188,10 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* sp = src + ((size_t)plane * N + j0) * M;
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
         const int t = fdiv(idx, M);
         pack_real(A, t, idx - t * M, M, sp[idx]);
@@ -208,10 +208,10 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
     // two lines per transform: Z = X_2p + i X_2p+1 (Hermitian extensions, DC / Nyquist bins taken real,
     // which is what the real part of one line's inverse keeps) -> z = x_2p + i x_2p+1
     const int P = (T + 1) / 2;
@@ -292,8 +292,8 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
-    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);   // T+1 lines
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);   // T+1 lines
     float* W1 = W0 + (size_t)(T + 1) * M;                       // T lines
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* xp = x + (size_t)plane * MN;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
         pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
     }
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
@@ -370,8 +370,8 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
-    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);
     float* W1 = W0 + (size_t)(T + 1) * M;
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const float* sp = s + (size_t)plane * 2 * MN;
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
         pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
     }
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);

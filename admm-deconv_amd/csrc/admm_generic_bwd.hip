@@ -68,8 +68,8 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
-    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);   // sbar_{k-1} ch0, T+1 lines
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);   // sbar_{k-1} ch0, T+1 lines
     float* W1 = W0 + (size_t)(T + 1) * M;                       // sbar_{k-1} ch1, T lines
     float* V = reinterpret_cast<float*>(smem_raw);              // vbar lines j0-1 .. j0+T (aliases A, B)
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
         pack_real(A, t, i, M, g);
     }
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
@@ -201,8 +201,8 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)T * M;
-    float* W0 = reinterpret_cast<float*>(B + (size_t)T * M);
+    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);
     float* W1 = W0 + (size_t)(T + 1) * M;
     const int plane = blockIdx.y, j0 = blockIdx.x * T;
     const size_t poff = (size_t)plane * 2 * MN;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
         pack_real(A, t, i, M, g);
     }
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * T * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
