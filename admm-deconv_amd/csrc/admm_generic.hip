@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
     float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const float* sp = src + ((size_t)plane * N + j0) * M;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
@@ -209,7 +210,8 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
     float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
     // two lines per transform: Z = X_2p + i X_2p+1 (Hermitian extensions, DC / Nyquist bins taken real,
@@ -218,11 +220,11 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
     for (int idx = threadIdx.x; idx < P * M; idx += blockDim.x) {
         const int p = fdiv(idx, M), k = idx - p * M;
         const float2* sa = sp + (size_t)(2 * p) * H;
-        float2 xa = k < H ? sa[k] : cconj(sa[M - k]);
-        float2 xb = make_float2(0.0f, 0.0f);
-        if (2 * p + 1 < T) xb = k < H ? sa[H + k] : cconj(sa[H + M - k]);
-        if (k == 0 || 2 * k == M) xa.y = xb.y = 0.0f;
-        A[idx] = make_float2(xa.x - xb.y, xa.y + xb.x);
+        float2 ev = k < H ? sa[k] : cconj(sa[M - k]);   // line 2p
+        float2 od = make_float2(0.0f, 0.0f);             // line 2p + 1
+        if (2 * p + 1 < T) od = k < H ? sa[H + k] : cconj(sa[H + M - k]);
+        if (k == 0 || 2 * k == M) ev.y = od.y = 0.0f;
+        A[idx] = make_float2(ev.x - od.y, ev.y + od.x);
     }
     __syncthreads();
     const float2* R = fft<true>(A, B, P, M, pM, tw);
@@ -248,7 +250,8 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
     const int N = pN.n;
     float2* A = reinterpret_cast<float2*>(smem_raw);
     float2* B = A + (size_t)KB * N;
-    const int plane = blockIdx.y, k0 = blockIdx.x * KB;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, k0 = xb.x * KB;
     const int kc = min(KB, H - k0);
     const float2* sp = src + (size_t)plane * N * H + k0;
     float2* dp = dst + (size_t)plane * N * H + k0;
@@ -295,7 +298,8 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
     float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
     float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);   // T+1 lines
     float* W1 = W0 + (size_t)(T + 1) * M;                       // T lines
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const float* xp = x + (size_t)plane * MN;
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
@@ -373,7 +377,8 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
     float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
     float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);
     float* W1 = W0 + (size_t)(T + 1) * M;
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const float* sp = s + (size_t)plane * 2 * MN;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;

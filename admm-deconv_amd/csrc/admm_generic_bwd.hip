@@ -72,7 +72,8 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);   // sbar_{k-1} ch0, T+1 lines
     float* W1 = W0 + (size_t)(T + 1) * M;                       // sbar_{k-1} ch1, T lines
     float* V = reinterpret_cast<float*>(smem_raw);              // vbar lines j0-1 .. j0+T (aliases A, B)
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const size_t poff = (size_t)plane * 2 * MN;
     const float* vp = vb + (size_t)plane * MN;
     for (int idx = threadIdx.x; idx < (T + 2) * M; idx += blockDim.x) {
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
             sb_out[poff + MN + o] = n1;
         }
     }
-    block_pair(racc, tacc, part + 2 * ((size_t)plane * gridDim.x + blockIdx.x));
+    block_pair(racc, tacc, part + 2 * ((size_t)plane * gridDim.x + xb.x));
     if (!s1p) return;
     __syncthreads();   // W0/W1 complete; V (aliasing A, B) is dead
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
@@ -204,7 +205,8 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
     float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
     float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);
     float* W1 = W0 + (size_t)(T + 1) * M;
-    const int plane = blockIdx.y, j0 = blockIdx.x * T;
+    const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
+    const int plane = xb.y, j0 = xb.x * T;
     const size_t poff = (size_t)plane * 2 * MN;
     for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
         const int t = fdiv(idx, M), i = idx - t * M;
