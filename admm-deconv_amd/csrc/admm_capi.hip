@@ -412,7 +412,9 @@ int gen_T(int M, int N) {
     return 1;
 }
 int gen_KB(int M, int N) {
-    int kb = gen_env("ADMM_GEN_KN", 2048) / N;
+    // 1024 points per column block: with the XCD-aware block order, smaller blocks won at every size
+    // measured (480x640 column pass 3.29 -> 2.92 ms; 256 / 512 / 2048+ slower, tools/time_generic.py)
+    int kb = gen_env("ADMM_GEN_KN", 1024) / N;
     kb = kb < 1 ? 1 : (kb > 16 ? 16 : kb);
     return kb > M / 2 + 1 ? M / 2 + 1 : kb;
 }
