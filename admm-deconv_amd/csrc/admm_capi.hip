@@ -489,7 +489,10 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     }
     const int T = line_T(M, N);
     const int KB = column_KB(M, N);
-    const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    // the per-iteration line update runs 4-line blocks at 512-point lines (its just-in-time loads let 4 of
+    // them share a CU, admm_kernels.hip line_kernel); the one-off line transforms keep T
+    const int Tu = (M == 512 && T > 4) ? 4 : T;
+    const size_t llds = line_lds(M, Tu), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
     float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
     const size_t np = planes;
@@ -526,7 +529,8 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 sn = (it & 1) ? sbuf[0] : sbuf[1];
             }
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, hty, twM, N, tau, rho, it == 1 ? 1 : 0);
+                launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, hty, twM, N, tau, rho,
+                            it == 1 ? 1 : 0);
             });
         } else if (it < maxit) {
             // isotropic: s is written in place (no halo reads of s in ISO_A); with a trajectory each

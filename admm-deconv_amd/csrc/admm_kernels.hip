@@ -464,33 +464,45 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     float* sn = s_new + (size_t)plane * 2 * MN;
     const float* hp = hty + (size_t)plane * MN;
 
-    // ---- issue every global load of the block up front ----
+    // ---- issue every global load of the block up front -- except at 512-point lines (kJit): there the
+    // s / H^T y loads go just before their use, which cuts the registers held across the irFFT (156 -> 88
+    // VGPRs) so that 4-line blocks run 4 per CU (c4 line pass 1.173 -> 1.140 ms); at 256
+    // points the early loads win (0.192 vs 0.201 ms) ----
+    constexpr bool kJit = L == 256;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
     float4 pre0[NIT], pre1[NIT];
+    auto load_s = [&] {
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-        const int idx = tid + it * kThreads;
-        const int t = idx / M4;
-        const int i = (idx - t * M4) * 4;
-        const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
-        pre0[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-        pre1[it] = pre0[it];
-        if (!s_zero && idx < NE) {
-            pre0[it] = *reinterpret_cast<const float4*>(so + off);
-            if (t < T) pre1[it] = *reinterpret_cast<const float4*>(so + MN + off);
+        for (int it = 0; it < NIT; ++it) {
+            const int idx = tid + it * kThreads;
+            const int t = idx / M4;
+            const int i = (idx - t * M4) * 4;
+            const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
+            pre0[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            pre1[it] = pre0[it];
+            if (!s_zero && idx < NE) {
+                pre0[it] = *reinterpret_cast<const float4*>(so + off);
+                if (t < T) pre1[it] = *reinterpret_cast<const float4*>(so + MN + off);
+            }
         }
-    }
+    };
     float2 preh[NITF][RF];
+    auto load_h = [&] {
 #pragma unroll
-    for (int it = 0; it < NITF; ++it) {
-        const int idx = tid + it * kThreads;
-        const int f = idx / QF, j = idx - f * QF;
-        if (idx < T * QF) {
-            const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
+        for (int it = 0; it < NITF; ++it) {
+            const int idx = tid + it * kThreads;
+            const int f = idx / QF, j = idx - f * QF;
+            if (idx < T * QF) {
+                const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
 #pragma unroll
-            for (int r = 0; r < RF; ++r) preh[it][r] = hl[j + r * QF];
+                for (int r = 0; r < RF; ++r) preh[it][r] = hl[j + r * QF];
+            }
         }
+    };
+    if constexpr (!kJit) {
+        load_s();
+        load_h();
     }
     __syncthreads();
 
@@ -515,6 +527,10 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     const float* x = reinterpret_cast<const float*>(Xr);
     float* W0 = reinterpret_cast<float*>(Xr == X ? Bf : X);   // T+1 lines
     float* W1 = reinterpret_cast<float*>(Cf);                 // T lines
+    if constexpr (kJit) {
+        load_s();
+        load_h();
+    }
 
     // ---- s = Dx + u_old ; w = z - u   (ops.jl:169-173) ----
 #pragma unroll
