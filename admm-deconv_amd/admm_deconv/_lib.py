@@ -18,6 +18,11 @@ ADMM_E_WORKSPACE = -3
 ADMM_E_HIP = -4
 ADMM_E_REDUCER = -5
 
+# library options (admm_set_option, include/admm_deconv.h)
+OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER = range(7)
+OPTIONS = {"FUSED": OPT_FUSED, "FUSED_ADJ": OPT_FUSED_ADJ, "LINE_T": OPT_LINE_T, "COL_THREADS": OPT_COL_THREADS,
+           "GEN_TM": OPT_GEN_TM, "GEN_KN": OPT_GEN_KN, "PLANE_STAGGER": OPT_PLANE_STAGGER}
+
 K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE, K_ADJ = range(8)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
                   K_FINAL: "final", K_NORM: "norm", K_PLANE: "plane", K_ADJ: "adjoint"}
@@ -27,6 +32,8 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_tvd_backward_workspace_bytes", "admm_tvd_backward_f32",
            "admm_tvd_forward_sharded_f32", "admm_tvd_backward_sharded_f32",
            "admm_tvd_forward_record_f32", "admm_tvd_backward_recorded_f32",
+           "admm_tvd_forward_dev_f32", "admm_tvd_backward_dev_f32", "admm_tvd_forward_record_dev_f32",
+           "admm_tvd_backward_recorded_dev_f32", "admm_set_option", "admm_get_option",
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
 
@@ -87,6 +94,26 @@ def load():
                                               ctypes.POINTER(BatchReducer)]
     L.admm_tvd_backward_recorded_f32.restype = c_int
     L.admm_tvd_backward_recorded_f32.argtypes = list(L.admm_tvd_backward_sharded_f32.argtypes)
+    # device-resident lambda / rho (include/admm_deconv.h): same argument lists with two device pointers
+    # in place of the two floats, and a (nullable) reducer at the end
+    L.admm_tvd_forward_dev_f32.restype = c_int
+    L.admm_tvd_forward_dev_f32.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                           c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p,
+                                           ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_backward_dev_f32.restype = c_int
+    L.admm_tvd_backward_dev_f32.argtypes = [c_void_p] * 6 + [c_int] * 4 + [c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                                                             c_int, c_int, c_void_p, c_void_p, c_size_t,
+                                                                             c_void_p, ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_forward_record_dev_f32.restype = c_int
+    L.admm_tvd_forward_record_dev_f32.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                                  c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_size_t,
+                                                  c_void_p, ctypes.POINTER(BatchReducer)]
+    L.admm_tvd_backward_recorded_dev_f32.restype = c_int
+    L.admm_tvd_backward_recorded_dev_f32.argtypes = list(L.admm_tvd_backward_dev_f32.argtypes)
+    L.admm_set_option.restype = c_int
+    L.admm_set_option.argtypes = [c_int, c_int]
+    L.admm_get_option.restype = c_int
+    L.admm_get_option.argtypes = [c_int, ctypes.POINTER(c_int)]
     L.admm_metrics_workspace_bytes.restype = c_int
     L.admm_metrics_workspace_bytes.argtypes = [c_int] * 6 + [ctypes.POINTER(c_size_t)]
     L.admm_gmsd_f32.restype = c_int
@@ -140,3 +167,29 @@ def profile_get(cls):
     n = ctypes.c_longlong(0)
     check(load().admm_profile_get(int(cls), ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+def set_option(opt, value):
+    """admm_set_option: `opt` is an OPT_* index or a name from OPTIONS ("FUSED", "LINE_T", ...)."""
+    check(load().admm_set_option(OPTIONS[opt] if isinstance(opt, str) else int(opt), int(value)))
+
+
+def get_option(opt):
+    v = ctypes.c_int(0)
+    check(load().admm_get_option(OPTIONS[opt] if isinstance(opt, str) else int(opt), ctypes.byref(v)))
+    return v.value
+
+
+class option:
+    """Context manager: `with option("FUSED", 0): ...` sets a library option and restores it."""
+
+    def __init__(self, opt, value):
+        self.opt, self.value = opt, value
+
+    def __enter__(self):
+        self.old = get_option(self.opt)
+        set_option(self.opt, self.value)
+        return self
+
+    def __exit__(self, *a):
+        set_option(self.opt, self.old)

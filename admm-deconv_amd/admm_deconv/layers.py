@@ -11,8 +11,11 @@ are trainable (`Flux.@layer ... trainable=`, deconv_admm.jl:55,107,161,209) and 
 
 Here the parameters are torch tensors on a ROCm device and `tvd_fft` is the HIP solve behind the
 C ABI.  Shapes follow the rule "torch shape = reversed Julia shape": Julia weight (kh,kw,1,1) is
-torch (1,1,kw,kh); Julia input (M,N,P,B) is torch (B,P,N,M).  This round mirrors the forward
-(inference); the Zygote adjoint (BASELINE config c5) is the next step.
+torch (1,1,kw,kh); Julia input (M,N,P,B) is torch (B,P,N,M).  λ and ρ stay on the device: the
+projection clamps them in place there and the solve reads them in-kernel (admm_tvd_forward_dev_f32),
+so neither the forward nor the backward reads them back to the host.  Under autograd the layer is
+differentiable in (x, weight, λ, ρ) through the HIP adjoint of the K unrolled iterations (what Zygote
+computes for the reference's training step, src/train.jl:51; BASELINE config c5).
 """
 from __future__ import annotations
 
@@ -113,9 +116,9 @@ class Admm:
             self.weight.clamp_(0.0, 1.0)                         # :219
 
     def __call__(self, x, scalars=None):
-        """(d::Admm)(x) -- deconv_admm.jl:215-225.  scalars: host (lambda, rho) of the already projected
-        layer (Parallel reads every branch's pair with one device-to-host copy); None = project and
-        read them here."""
+        """(d::Admm)(x) -- deconv_admm.jl:215-225.  λ and ρ are passed to the solve as device tensors
+        (read in-kernel, no host sync).  scalars: optional host (lambda, rho) of the already projected
+        layer, used instead of the device values."""
         if scalars is None:
             self.project()
         h = self.weight if self.weight.numel() > 0 else None
@@ -229,28 +232,14 @@ class Parallel:
             return self.connection(*[L(x) for L in self.layers])
         cur = torch.cuda.current_stream(x.device)
         side = self._side_streams(x.device)
-        # project every ADMM branch and read all (lambda, rho) pairs with ONE device-to-host copy: the
-        # C ABI takes them by value, and a per-branch read would block the host behind the branches
-        # already queued
-        adm = [isinstance(L, Admm) for L in self.layers]
-        host = None
-        if any(adm):
-            for L, a in zip(self.layers, adm):
-                if a:
-                    L.project()
-            host = torch.cat([torch.cat([L.lam.detach().reshape(1), L.rho.detach().reshape(1)])
-                              for L, a in zip(self.layers, adm) if a]).cpu().tolist()
+        # each ADMM branch projects its λ / ρ / PSF in place on its own stream and the solve reads them
+        # in-kernel: nothing here waits for the device
         outs = []
-        i = 0
-        for L, a, st in zip(self.layers, adm, side):
+        for L, st in zip(self.layers, side):
             x.record_stream(st)     # read on st (forward, and by the adjoint on st after the join)
             st.wait_stream(cur)
             with torch.cuda.stream(st):
-                if a:
-                    outs.append(L(x, scalars=(host[2 * i], host[2 * i + 1])))
-                    i += 1
-                else:
-                    outs.append(L(x))
+                outs.append(L(x))
         for o, st in zip(outs, side):
             cur.wait_stream(st)
             o.record_stream(cur)    # allocated on st, consumed on the caller's stream

@@ -23,20 +23,37 @@ __all__ = ["tvd_fft", "tvd_fft_backward", "tvd_fft_record", "tvd_fft_backward_re
 
 
 class Workspace:
-    """Caller-owned device scratch for the solve (the library allocates nothing)."""
+    """Caller-owned device scratch for the solve (the library allocates nothing).
+
+    A workspace serves one stream at a time: the solve's scratch state (C table, H^T y, s, spectra)
+    lives in it for the whole enqueued solve.  `get(nbytes, device, stream)` marks the buffer as used on
+    `stream`, so that a reallocation (or dropping the workspace) does not hand the memory to other work
+    before that stream has finished with it."""
 
     def __init__(self):
         self._buf = None
 
-    def get(self, nbytes, device):
+    def get(self, nbytes, device, stream=None):
         if self._buf is None or self._buf.numel() < nbytes or self._buf.device != device:
             self._buf = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
+        if stream is not None and isinstance(stream, torch.cuda.Stream) and stream != torch.cuda.current_stream(device):
+            self._buf.record_stream(stream)
         ptr = self._buf.data_ptr()
         off = (-ptr) % 256
         return ptr + off, self._buf.numel() - off
 
 
+# default workspaces, one per (kind, device, stream): concurrent solves on different streams (e.g. the
+# branches of layers.Parallel) must not share scratch state
 _default_ws = {}
+
+
+def _default_workspace(kind, device, stream):
+    return _default_ws.setdefault((kind, device, _stream_handle(stream)), Workspace())
+
+
+def _stream_handle(stream):
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
 
 
 def _make_reducer(workspace, group):
@@ -78,6 +95,43 @@ def _sharded(isotropic, group):
     return dist.is_initialized() and dist.get_world_size(group) > 1
 
 
+class _DevScalars:
+    """lambda / rho as device fp32 1-element tensors (the reference's `λ::CGPUArray`, ops.jl:99,181): the
+    library reads them in-kernel, so the call needs no device-to-host read.  Holds the (possibly
+    converted) tensors alive; `ptrs` are their device addresses."""
+
+    __slots__ = ("lam", "rho")
+
+    def __init__(self, lam, rho, device, stream):
+        self.lam = self._one(lam, "lambda", device)
+        self.rho = self._one(rho, "rho", device)
+        if stream is not None and isinstance(stream, torch.cuda.Stream) and stream != torch.cuda.current_stream(device):
+            for t in (self.lam, self.rho):
+                t.record_stream(stream)
+
+    @staticmethod
+    def _one(v, name, device):
+        if isinstance(v, torch.Tensor):
+            if v.numel() != 1:
+                raise ValueError(f"{name} must have exactly one element (reference uses 1-element vectors)")
+            t = v.detach().reshape(1)
+            if t.device != device:
+                if t.device.type == "cuda":
+                    raise ValueError(f"{name} is on {t.device}, the solve on {device}")
+                t = t.to(device)            # host tensor: one (blocking) upload
+            return t.to(torch.float32).contiguous()
+        # a host number next to a device tensor: a fill on the device, no transfer
+        return torch.full((1,), _scalar(v, name), dtype=torch.float32, device=device)
+
+    @property
+    def ptrs(self):
+        return self.lam.data_ptr(), self.rho.data_ptr()
+
+
+def _on_device(lam, rho):
+    return any(isinstance(v, torch.Tensor) and v.device.type == "cuda" for v in (lam, rho))
+
+
 def _scalar(v, name):
     if isinstance(v, torch.Tensor):
         if v.numel() != 1:
@@ -93,13 +147,20 @@ def _scalar(v, name):
     return v
 
 
+def _stream_of(stream, device):
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    return stream, _stream_handle(stream)
+
+
 def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, workspace=None, stream=None,
                  group=None):
     """ADMM TV deconvolution of every (M x N) plane of y (ops.jl:181).
 
     y:    torch float32 tensor (B, P, N, M) on a ROCm device (Julia (M,N,P,B)); a 2-D (N, M) or
           3-D (P, N, M) tensor is treated as B = 1 (and P = 1).
-    lam, rho: scalars or 1-element tensors (the reference's 1-element vectors; default ρ = [1]).
+    lam, rho: host scalars, or 1-element tensors (the reference's 1-element vectors; default ρ = [1]).
+          Device tensors are read in-kernel (admm_tvd_forward_dev_f32): no host synchronisation.
     h:    PSF tensor (kw, kh) (Julia (kh,kw,1,1)), or None / empty for the reference's empty PSF.
     Returns a new tensor x of y's shape (y is not modified)."""
     if not isinstance(y, torch.Tensor) or y.device.type != "cuda":
@@ -117,8 +178,6 @@ def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=Non
         raise ValueError("tvd_fft: y must be 2-D, 3-D or 4-D")
     y4 = y4.contiguous()
     B, P, N, M = y4.shape
-    lam = _scalar(lam, "lambda")
-    rho = _scalar(rho, "rho")
     if h is None or (isinstance(h, torch.Tensor) and h.numel() == 0):
         hp, kh, kw, hbuf = None, 0, 0, None
     else:
@@ -134,23 +193,26 @@ def _forward_raw(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=Non
         out = torch.empty_like(y4)
     elif out.shape != y4.shape or out.dtype != torch.float32 or not out.is_contiguous() or out.device != y.device:
         raise ValueError("out must be a contiguous float32 tensor of y's shape on y's device")
+    stream, s_handle = _stream_of(stream, y.device)
     nbytes = _lib.workspace_bytes(M, N, P, B, kh, kw, isotropic)
     if workspace is None:
-        workspace = _default_ws.setdefault(y.device, Workspace())
-    ws_ptr, ws_len = workspace.get(nbytes, y.device)
-    if stream is None:
-        stream = torch.cuda.current_stream(y.device)
-    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
-    if _sharded(isotropic, group):
-        red, keep = _make_reducer(workspace, group)
+        workspace = _default_workspace("fwd", y.device, stream)
+    ws_ptr, ws_len = workspace.get(nbytes, y.device, stream)
+    red, keep = _make_reducer(workspace, group) if _sharded(isotropic, group) else (None, None)
+    if _on_device(lam, rho):
+        dv = _DevScalars(lam, rho, y.device, stream)
+        _lib.check(_lib.load().admm_tvd_forward_dev_f32(
+            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, *dv.ptrs, int(bool(isotropic)), int(maxit),
+            ws_ptr, ws_len, s_handle, ctypes.byref(red) if red is not None else None))
+    elif red is not None:
         _lib.check(_lib.load().admm_tvd_forward_sharded_f32(
-            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, 1, int(maxit),
-            ws_ptr, ws_len, s_handle, ctypes.byref(red)))
-        del keep
+            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, _scalar(lam, "lambda"), _scalar(rho, "rho"), 1,
+            int(maxit), ws_ptr, ws_len, s_handle, ctypes.byref(red)))
     else:
         _lib.check(_lib.load().admm_tvd_forward_f32(
-            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, lam, rho, int(bool(isotropic)), int(maxit),
-            ws_ptr, ws_len, s_handle))
+            y4.data_ptr(), out.data_ptr(), M, N, P, B, hp, kh, kw, _scalar(lam, "lambda"), _scalar(rho, "rho"),
+            int(bool(isotropic)), int(maxit), ws_ptr, ws_len, s_handle))
+    del keep
     return out.reshape(shape)
 
 
@@ -167,6 +229,13 @@ def _prep(y, h):
     return shape, y4, hb.to(device=y.device, dtype=torch.float32).contiguous()
 
 
+def _scalars_for(lam, rho, device, stream):
+    """(device holder or None, host lambda, host rho): device tensors stay on the device."""
+    if _on_device(lam, rho):
+        return _DevScalars(lam, rho, device, stream), None, None
+    return None, _scalar(lam, "lambda"), _scalar(rho, "rho")
+
+
 def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, workspace=None,
                      stream=None, group=None):
     """Adjoint of tvd_fft through all `maxit` unrolled iterations (what Zygote computes for the
@@ -177,30 +246,30 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     shape, y4, hb = _prep(y, h)
     B, P, N, M = y4.shape
     xb = x_bar.reshape(y4.shape).to(torch.float32).contiguous()
-    lam = _scalar(lam, "lambda")
-    rho = _scalar(rho, "rho")
     kw, kh = (0, 0) if hb is None else hb.shape
     want_h = need_h and hb is not None
+    stream, s_handle = _stream_of(stream, y.device)
+    dv, lam_h, rho_h = _scalars_for(lam, rho, y.device, stream)
     nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, want_h)
     if workspace is None:
-        workspace = _default_ws.setdefault(("bwd", y.device), Workspace())
-    ws_ptr, ws_len = workspace.get(nbytes, y.device)
-    if stream is None:
-        stream = torch.cuda.current_stream(y.device)
-    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        workspace = _default_workspace("bwd", y.device, stream)
+    ws_ptr, ws_len = workspace.get(nbytes, y.device, stream)
     x = torch.empty_like(y4)
     y_bar = torch.empty_like(y4)
     h_bar = torch.empty_like(hb) if want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y.device)
-    args = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
-            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, lam, rho,
-            int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle)
-    if _sharded(isotropic, group):
-        red, keep = _make_reducer(workspace, group)
-        _lib.check(_lib.load().admm_tvd_backward_sharded_f32(*args, ctypes.byref(red)))
-        del keep
+    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
+            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
+    tail = (int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle)
+    red, keep = _make_reducer(workspace, group) if _sharded(isotropic, group) else (None, None)
+    L = _lib.load()
+    if dv is not None:
+        _lib.check(L.admm_tvd_backward_dev_f32(*head, *dv.ptrs, *tail, ctypes.byref(red) if red is not None else None))
+    elif red is not None:
+        _lib.check(L.admm_tvd_backward_sharded_f32(*head, lam_h, rho_h, *tail, ctypes.byref(red)))
     else:
-        _lib.check(_lib.load().admm_tvd_backward_f32(*args))
+        _lib.check(L.admm_tvd_backward_f32(*head, lam_h, rho_h, *tail))
+    del keep
     return x.reshape(shape), y_bar.reshape(shape), h_bar, scal[0], scal[1]
 
 
@@ -210,31 +279,34 @@ class Recording:
     once (no recompute in the backward).  Memory: about 8 B/px per iteration (plus 8 B/px of dim-2
     spectra per iteration with a PSF when h_bar is needed) -- sized for MI355X's 288 GB HBM."""
 
-    __slots__ = ("workspace", "y4", "hb", "shape", "lam", "rho", "iso", "maxit", "want_h", "group", "dims")
+    __slots__ = ("workspace", "y4", "hb", "shape", "dv", "lam", "rho", "iso", "maxit", "want_h", "group", "dims")
 
 
 def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, stream=None, group=None):
-    """Forward solve that records its trajectory.  Returns (x, Recording); see tvd_fft_backward_recorded."""
+    """Forward solve that records its trajectory.  Returns (x, Recording); see tvd_fft_backward_recorded.
+    lam / rho as device tensors are read in-kernel (no host sync), as in tvd_fft."""
     shape, y4, hb = _prep(y, h)
     B, P, N, M = y4.shape
+    stream, s_handle = _stream_of(stream, y.device)
     rec = Recording()
-    rec.lam, rec.rho = _scalar(lam, "lambda"), _scalar(rho, "rho")
+    rec.dv, rec.lam, rec.rho = _scalars_for(lam, rho, y.device, stream)
     kw, kh = (0, 0) if hb is None else hb.shape
     rec.want_h = bool(need_h and hb is not None)
     rec.y4, rec.hb, rec.shape, rec.iso, rec.maxit, rec.group = y4, hb, shape, bool(isotropic), int(maxit), group
     rec.dims = (M, N, P, B, kh, kw)
     nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, rec.want_h)
     rec.workspace = Workspace()
-    ws_ptr, ws_len = rec.workspace.get(nbytes, y.device)
-    if stream is None:
-        stream = torch.cuda.current_stream(y.device)
-    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    ws_ptr, ws_len = rec.workspace.get(nbytes, y.device, stream)
     x = torch.empty_like(y4)
     red, keep = _make_reducer(rec.workspace, group) if _sharded(isotropic, group) else (None, None)
-    _lib.check(_lib.load().admm_tvd_forward_record_f32(
-        y4.data_ptr(), x.data_ptr(), M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, rec.lam, rec.rho,
-        int(rec.iso), rec.maxit, int(rec.want_h), ws_ptr, ws_len, s_handle,
-        ctypes.byref(red) if red is not None else None))
+    head = (y4.data_ptr(), x.data_ptr(), M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
+    tail = (int(rec.iso), rec.maxit, int(rec.want_h), ws_ptr, ws_len, s_handle,
+            ctypes.byref(red) if red is not None else None)
+    L = _lib.load()
+    if rec.dv is not None:
+        _lib.check(L.admm_tvd_forward_record_dev_f32(*head, *rec.dv.ptrs, *tail))
+    else:
+        _lib.check(L.admm_tvd_forward_record_f32(*head, rec.lam, rec.rho, *tail))
     del keep
     return x.reshape(shape), rec
 
@@ -251,21 +323,25 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None):
     x4 = x.reshape(y4.shape)
     if not x4.is_contiguous():
         raise ValueError("x must be the recorded forward's (contiguous) output")
+    stream, s_handle = _stream_of(stream, y4.device)
     ws = rec.workspace
-    ws_ptr = ws._buf.data_ptr() + (-ws._buf.data_ptr()) % 256
-    ws_len = ws._buf.numel() - (-ws._buf.data_ptr()) % 256
-    if stream is None:
-        stream = torch.cuda.current_stream(y4.device)
-    s_handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    ws_ptr, ws_len = ws.get(0, y4.device, stream)
     y_bar = torch.empty_like(y4)
     h_bar = torch.empty_like(hb) if rec.want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y4.device)
     red, keep = _make_reducer(ws, rec.group) if _sharded(rec.iso, rec.group) else (None, None)
-    _lib.check(_lib.load().admm_tvd_backward_recorded_f32(
-        y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
-        scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw, rec.lam, rec.rho,
-        int(rec.iso), rec.maxit, x4.data_ptr(), ws_ptr, ws_len, s_handle,
-        ctypes.byref(red) if red is not None else None))
+    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
+            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
+    tail = (int(rec.iso), rec.maxit, x4.data_ptr(), ws_ptr, ws_len, s_handle,
+            ctypes.byref(red) if red is not None else None)
+    L = _lib.load()
+    if rec.dv is not None:
+        if stream != torch.cuda.current_stream(y4.device):
+            for t in (rec.dv.lam, rec.dv.rho):
+                t.record_stream(stream)
+        _lib.check(L.admm_tvd_backward_recorded_dev_f32(*head, *rec.dv.ptrs, *tail))
+    else:
+        _lib.check(L.admm_tvd_backward_recorded_f32(*head, rec.lam, rec.rho, *tail))
     del keep
     rec.workspace = None    # released once the stream has consumed it (caching allocator is stream-ordered)
     return y_bar.reshape(rec.shape), h_bar, scal[0], scal[1]
@@ -277,17 +353,20 @@ class _TvdFFTFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, lam_t, rho_t, h_t, isotropic, maxit, group, scalars):
-        # the forward records its trajectory; the backward runs only the reverse sweep from it
+        # the forward records its trajectory; the backward runs only the reverse sweep from it.  lam_t / rho_t
+        # (device tensors) are read in-kernel unless the caller handed their host values in `scalars`
         need_h = h_t.numel() > 0 and ctx.needs_input_grad[3]
         lam, rho = scalars if scalars is not None else (lam_t, rho_t)
         x, ctx.rec = tvd_fft_record(y, lam, rho, h_t if h_t.numel() else None, isotropic, maxit,
                                     need_h=need_h, group=group)
-        ctx.save_for_backward(lam_t, rho_t, h_t, x)   # x: version-checked (must stay unmodified)
+        # y (read again by the reverse sweep's h_bar correlation) and x are version-checked: an in-place
+        # change of either between forward and backward raises instead of giving a wrong gradient
+        ctx.save_for_backward(y, lam_t, rho_t, h_t, x)
         return x
 
     @staticmethod
     def backward(ctx, x_bar):
-        lam_t, rho_t, h_t, x = ctx.saved_tensors
+        _y, lam_t, rho_t, h_t, x = ctx.saved_tensors
         need_h = ctx.rec.want_h
         yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar)
         ctx.rec = None
@@ -304,20 +383,21 @@ def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, wo
             group=None, scalars=None):
     """ADMM TV deconvolution of every (M x N) plane of y -- src/ops/ops.jl:181 semantics.
 
-    y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: scalars or
-    1-element tensors; h: PSF (kw,kh) (= Julia (kh,kw)) or None/empty.  Returns a new tensor.
+    y: float32 tensor (B,P,N,M) on a ROCm device (= Julia (M,N,P,B)); lam, rho: host scalars or
+    1-element tensors -- device tensors (the reference's `λ::CGPUArray`) are read in-kernel, so the call
+    never synchronises the host; h: PSF (kw,kh) (= Julia (kh,kw)) or None/empty.  Returns a new tensor.
     Differentiable (y, lam, rho, h) when autograd is recording and any of them requires grad
     (either prox); the gradient is the exact adjoint of the K unrolled iterations.
     group: torch.distributed group the batch is sharded over (each rank passes its own slice).  The
     isotropic prox's pixelnorm then spans the whole sharded batch (one M x N all-reduce per
     iteration), so every rank gets its slice of the unsharded result; ignored for the anisotropic
     prox, whose planes are independent.
-    scalars: optional host (lambda, rho) equal to the values of tensor lam / rho, so that the call does
-    not read them back from the device (a host sync); gradients still flow to the tensors."""
+    scalars: optional host (lambda, rho) equal to the values of tensor lam / rho, used instead of the
+    device values (gradients still flow to the tensors)."""
     tensors = [t for t in (y, lam, rho, h) if isinstance(t, torch.Tensor)]
     if torch.is_grad_enabled() and any(t.requires_grad for t in tensors):
         dev = y.device
-        as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.tensor([float(v)], device=dev)  # noqa: E731
+        as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.full((1,), float(v), device=dev)  # noqa: E731
         h_t = h if isinstance(h, torch.Tensor) else torch.zeros(0, device=dev)
         return _TvdFFTFn.apply(y, as_t(lam), as_t(rho), h_t, bool(isotropic), int(maxit), group, scalars)
     if scalars is not None:

@@ -15,7 +15,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-__all__ = ["shard_range", "solve_sharded"]
+__all__ = ["shard_range", "solve_sharded", "ShardGather"]
 
 
 def shard_range(total, world, rank):
@@ -46,3 +46,91 @@ def solve_sharded(y_local, solve, *, gather="none", total=None, group=None):
         dist.gather(x_local.contiguous(), parts, dst=0, group=group)
         return torch.cat(parts) if rank == 0 else None
     raise ValueError(f"unknown gather mode {gather!r}")
+
+
+class ShardGather:
+    """Batch-sharded solve with the output gather to rank `dst` overlapped with compute (BASELINE c3:
+    2048 images of 256x256 sharded over the GPUs of a node, "RCCL gather").
+
+    Every `step()` solves this rank's shard y_local (in `chunks` slices, `solve(y_slice, out_slice)`)
+    into one of two output buffers and gathers each slice to rank `dst` as soon as it is solved.  On a
+    ROCm device with backend "nccl" (RCCL over xGMI) the gathers run on their own stream: slice c's
+    gather waits only for slice c's solve, and the next step's solve (into the other buffer) does not
+    wait for this step's gathers -- it waits only for the gathers that read the buffer it is about to
+    overwrite (two steps back).  So the xGMI transfer of one batch overlaps the solve of the next.
+    With "gloo" (CPU collectives: the multi-process tests) the same schedule runs synchronously,
+    CUDA slices going through host copies.
+
+    `gathered()` returns rank dst's (world * B_local, ...) result of the last step (None elsewhere);
+    call it after the device work has completed (torch.cuda.synchronize or `wait()`)."""
+
+    def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0):
+        self.y = y_local
+        self.solve = solve
+        self.group = group
+        self.dst = dst
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        n = y_local.shape[0]
+        chunks = max(1, min(int(chunks), n))
+        self.bounds = [shard_range(n, chunks, c) for c in range(chunks)]
+        self.out = [torch.empty_like(y_local) for _ in range(2)]
+        self.cuda = y_local.is_cuda
+        self.gloo = self.world > 1 and dist.get_backend(group) == "gloo"
+        self.async_comm = self.cuda and self.world > 1 and not self.gloo
+        if self.world > 1 and self.rank == dst:
+            full = (self.world * n,) + tuple(y_local.shape[1:])
+            dev = "cpu" if self.gloo else y_local.device
+            self.recv = torch.empty(full, dtype=y_local.dtype, device=dev)
+        else:
+            self.recv = None
+        if self.async_comm:
+            self.comm = torch.cuda.Stream(device=y_local.device)
+            self.freed = [None, None]      # event: the gathers reading out[b] have completed
+        self.i = 0
+
+    def _parts(self, c):
+        """rank dst's receive views for chunk c of every rank (rank r's chunk lands at r * n + start)."""
+        if self.recv is None:
+            return None
+        n = self.y.shape[0]
+        s, k = self.bounds[c]
+        return [self.recv[r * n + s: r * n + s + k] for r in range(self.world)]
+
+    def step(self):
+        b = self.i & 1
+        out = self.out[b]
+        if self.async_comm and self.freed[b] is not None:
+            torch.cuda.current_stream(self.y.device).wait_event(self.freed[b])
+        for c, (s, k) in enumerate(self.bounds):
+            self.solve(self.y[s:s + k], out[s:s + k])
+            if self.world == 1:
+                continue
+            if self.async_comm:
+                done = torch.cuda.Event()
+                done.record(torch.cuda.current_stream(self.y.device))
+                with torch.cuda.stream(self.comm):
+                    self.comm.wait_event(done)
+                    dist.gather(out[s:s + k], self._parts(c), dst=self.dst, group=self.group)
+            else:
+                src = out[s:s + k].cpu() if (self.gloo and self.cuda) else out[s:s + k]
+                dist.gather(src, self._parts(c), dst=self.dst, group=self.group)
+        if self.async_comm:
+            ev = torch.cuda.Event()
+            ev.record(self.comm)
+            self.freed[b] = ev
+        self.i += 1
+
+    def wait(self):
+        """Make the caller's stream wait for every gather issued so far."""
+        if self.async_comm:
+            torch.cuda.current_stream(self.y.device).wait_stream(self.comm)
+
+    def local(self):
+        """This rank's solved shard from the last step."""
+        return self.out[(self.i - 1) & 1]
+
+    def gathered(self):
+        if self.world == 1:
+            return self.local()
+        return self.recv

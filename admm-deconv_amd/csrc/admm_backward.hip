@@ -81,8 +81,9 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
                                                             const float* __restrict__ sb_in, float* __restrict__ sb_out,
                                                             float* __restrict__ vsum, float2* __restrict__ spec0,
                                                             double* __restrict__ part, const float2* __restrict__ twM,
-                                                            int N, float tau, float rho, int first_k /*k==1*/,
+                                                            int N, const float* __restrict__ prm, int first_k /*k==1*/,
                                                             int last_k /*k==K*/) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -367,8 +368,9 @@ __global__ void reduce_planes_kernel(const float* __restrict__ Qp, double* __res
 
 // Final assembly of the scalar / PSF gradients into the caller's fp32 outputs.
 __global__ void grads_final_kernel(const double* __restrict__ rt, const double* __restrict__ hb_corr,
-                                   const double* __restrict__ hb_A, int ntaps, float lam, float rho,
+                                   const double* __restrict__ hb_A, int ntaps, const float* __restrict__ prm,
                                    float* __restrict__ lam_bar, float* __restrict__ rho_bar, float* __restrict__ h_bar) {
+    const float lam = prm[2]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
         const double tau_bar = rt[1];
@@ -400,8 +402,9 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                                                              const float* __restrict__ sb_in, float* __restrict__ vbar_out,
                                                              float* __restrict__ vsum, float* __restrict__ rpartial,
                                                              double* __restrict__ part, const float2* __restrict__ twM,
-                                                             int N, int planes, int G, float tau, float rho,
+                                                             int N, int planes, int G, const float* __restrict__ prm,
                                                              int first_k, int last_k) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     // nrm1 = Nrm_{k-1} (k >= 2), nrm0 = Nrm_{k-2} (k >= 3; for D x_k = s_k - psi(s_{k-1}) we need f_{k-1}
     // only: nrm0 is unused but kept for symmetry of the call -- psi(s_{k-1}) uses nrm1)
     (void)nrm0;
@@ -546,7 +549,8 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
 // R map = sum over plane groups of the partial sums; tau_bar partials (block-reduced, one pair per block)
 __global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __restrict__ rpartial, float* __restrict__ Rmap,
                                                              const float* __restrict__ nrm1, int ngroups, size_t MN,
-                                                             float tau, double* __restrict__ part) {
+                                                             const float* __restrict__ prm, double* __restrict__ part) {
+    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
     __shared__ double red[2 * (kThreads / 64)];
     __shared__ float gred[kThreads];
     float tacc = 0.0f;
@@ -568,7 +572,8 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
                                                              const float* __restrict__ sk1, const float* __restrict__ nrm1,
                                                              const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                              float2* __restrict__ spec0, const float2* __restrict__ twM,
-                                                             int N, float tau, float rho) {
+                                                             int N, const float* __restrict__ prm) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;

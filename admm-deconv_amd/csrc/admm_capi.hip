@@ -13,8 +13,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
+#include <unordered_map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/admm_deconv.h"
@@ -53,7 +56,7 @@ int fail(int code, const char* fmt, ...) {
 bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 struct Layout {
-    size_t twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, xg, total;
+    size_t prm, twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, xg, total;
 };
 
 // The tuned kernels cover power-of-two 4 <= M <= 1024, 2 <= N <= 1024; every other shape from 2 x 2 up
@@ -62,18 +65,18 @@ bool pow2_shape(int M, int N) { return is_pow2(M) && is_pow2(N) && M >= 4 && M <
 bool generic_shape(int M, int N) { return !pow2_shape(M, N); }
 constexpr int kGenMax = 4096;
 
+// Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
+// choices; the others exist for tests (fused vs 2-pass) and tuning experiments.  A recording stores
+// the option values it was made with, and its replay rejects a change (RecTag below).
+std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}};
+int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
+
 // The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox;
-// ADMM_FUSED=0 forces the 2-pass path (tests compare the two).
+// ADMM_OPT_FUSED = 0 forces the 2-pass path (tests compare the two).
 bool fused_shape(int M, int N, bool iso) { return M == 256 && N == 256 && !iso; }
-bool fused_enabled() {
-    const char* e = getenv("ADMM_FUSED");
-    return !(e && e[0] == '0');
-}
-// ADMM_FUSED_ADJ=0 keeps the 2-pass reverse sweep (line_adj + column) on a fused trajectory
-bool fused_adj_enabled() {
-    const char* e = getenv("ADMM_FUSED_ADJ");
-    return !(e && e[0] == '0');
-}
+bool fused_enabled() { return opt(ADMM_OPT_FUSED) != 0; }
+// ADMM_OPT_FUSED_ADJ = 0 keeps the 2-pass reverse sweep (line_adj + column) on a fused trajectory
+bool fused_adj_enabled() { return opt(ADMM_OPT_FUSED_ADJ) != 0; }
 size_t fused_tables_bytes() { return admm::plane::tables_bytes(); }
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
@@ -97,6 +100,7 @@ Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
         return o;
     };
     const size_t MN = (size_t)M * N;
+    L.prm = take(16);   // {tau, rho, lambda} resolved on the device (setup_kernel / scal_kernel)
     L.twM = take((size_t)M * 8);
     L.twN = take((size_t)N * 8);
     L.C = take((size_t)(M / 2 + 1) * N * 4);
@@ -120,10 +124,8 @@ Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
 // T = lines per line-kernel block (power of two dividing N); KB = slots per column-kernel block.
 int line_T(int M, int N) {
     int pref = M <= 512 ? 8 : 4;
-    if (const char* e = getenv("ADMM_LINE_T")) {
-        int v = atoi(e);
-        if (v == 2 || v == 4 || v == 8 || v == 16) pref = v < pref ? v : pref;
-    }
+    const int v = opt(ADMM_OPT_LINE_T);
+    if (v == 2 || v == 4 || v == 8 || v == 16) pref = v < pref ? v : pref;
     return N < pref ? N : pref;
 }
 size_t line_lds(int M, int T) {
@@ -140,13 +142,11 @@ int max_q(int NN) {
     return NN;
 }
 // column block size: 1024 threads for long columns, so that a block covers >= 64 B of every row
-// (256 threads at N = 512 gave 4 slots = 32 B per row); ADMM_COL_THREADS overrides (256 or 1024)
+// (256 threads at N = 512 gave 4 slots = 32 B per row); ADMM_OPT_COL_THREADS overrides (256 or 1024)
 int column_threads(int N) {
     int nt = N >= 512 ? 1024 : 256;
-    if (const char* e = getenv("ADMM_COL_THREADS")) {
-        const int v = atoi(e);
-        if (v == 256 || (v == 1024 && N >= 256)) nt = v;
-    }
+    const int v = opt(ADMM_OPT_COL_THREADS);
+    if (v == 256 || (v == 1024 && N >= 256)) nt = v;
     return nt;
 }
 int column_KB(int M, int N) {
@@ -182,6 +182,9 @@ struct Launcher {
     hipStream_t s;
     bool prof;
     std::vector<PendingEv> ev;
+    // `launch` may return void or an int status: the template dispatchers (launch_line, launch_column,
+    // ...) return non-zero when no instance matches the requested tile, in which case nothing was
+    // enqueued and the call must fail instead of returning unwritten outputs.
     template <typename F>
     int run(int cls, F&& launch) {
         PendingEv p{cls, nullptr, nullptr};
@@ -190,13 +193,23 @@ struct Launcher {
             hipEventCreate(&p.b);
             hipEventRecord(p.a, s);
         }
-        launch();
-        hipError_t e = hipGetLastError();
+        int lrc = 0;
+        hipError_t e = hipSuccess;
+        using R = decltype(launch());
+        if constexpr (std::is_void_v<R>) {
+            launch();
+        } else if constexpr (std::is_same_v<R, hipError_t>) {
+            e = launch();   // the plane launchers report hipGetLastError() themselves
+        } else {
+            lrc = (int)launch();
+        }
+        if (e == hipSuccess) e = hipGetLastError();
         if (prof) {
             hipEventRecord(p.b, s);
             ev.push_back(p);
         }
         if (e != hipSuccess) return fail(ADMM_E_HIP, "kernel launch (class %d) failed: %s", cls, hipGetErrorString(e));
+        if (lrc != 0) return fail(ADMM_E_UNSUPPORTED, "no kernel instance for this tile (class %d, status %d)", cls, lrc);
         return ADMM_OK;
     }
     int finish() {
@@ -261,12 +274,12 @@ int launch_line_inv(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
 }
 
 int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float2* spec0,
-                const float* so, float* sn, const float* hty, const float2* twM, int N, float tau, float rho,
+                const float* so, float* sn, const float* hty, const float2* twM, int N, const float* prm,
                 int sz) {
 #define X(l, t)                                                                                          \
     if (L == l && T == t) {                                                                              \
         set_lds(line_kernel<l, t>, lds);                                                                 \
-        line_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, tau, rho, sz);    \
+        line_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz);    \
         return 0;                                                                                        \
     }
     ADMM_LT_CASES(X)
@@ -288,11 +301,11 @@ int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* 
 }
 
 int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* sn, const float* fmap,
-                 const float* hty, float2* spec0, const float2* twM, int N, float rho) {
+                 const float* hty, float2* spec0, const float2* twM, int N, const float* prm) {
 #define X(l, t)                                                                               \
     if (L == l && T == t) {                                                                   \
         set_lds(iso_b_kernel<l, t>, lds);                                                     \
-        iso_b_kernel<l, t><<<g, kThreads, lds, s>>>(sn, fmap, hty, spec0, twM, N, rho);      \
+        iso_b_kernel<l, t><<<g, kThreads, lds, s>>>(sn, fmap, hty, spec0, twM, N, prm);      \
         return 0;                                                                             \
     }
     ADMM_LT_CASES(X)
@@ -398,15 +411,14 @@ admm::gen::FPlan make_fplan(int n) {
     return p;
 }
 // lines per block: the largest of 8, 4, 2, 1 dividing N with T * M <= 4096 (LDS ~ 24 T M bytes)
-// experiment knobs: ADMM_GEN_TM (max T x M of a line block), ADMM_GEN_KN (max KB x N of a column block)
-int gen_env(const char* name, int dflt) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : 0;
+// options ADMM_OPT_GEN_TM (max T x M of a line block), ADMM_OPT_GEN_KN (max KB x N of a column block)
+int gen_opt(int k, int dflt) {
+    const int v = opt(k);
     return v >= 256 && v <= 8192 ? v : dflt;
 }
 int gen_T(int M, int N) {
     // 2048: smaller blocks, more of them resident per CU (480x640: 1.3x over 4096, tools/gen_knobs.sh)
-    const int tm = gen_env("ADMM_GEN_TM", 2048);
+    const int tm = gen_opt(ADMM_OPT_GEN_TM, 2048);
     for (int t = 8; t > 1; t >>= 1)
         if (N % t == 0 && t * M <= tm) return t;
     return 1;
@@ -414,7 +426,7 @@ int gen_T(int M, int N) {
 int gen_KB(int M, int N) {
     // 1024 points per column block: with the XCD-aware block order, smaller blocks won at every size
     // measured (480x640 column pass 3.29 -> 2.92 ms; 256 / 512 / 2048+ slower, tools/time_generic.py)
-    int kb = gen_env("ADMM_GEN_KN", 1024) / N;
+    int kb = gen_opt(ADMM_OPT_GEN_KN, 1024) / N;
     kb = kb < 1 ? 1 : (kb > 16 ? 16 : kb);
     return kb > M / 2 + 1 ? M / 2 + 1 : kb;
 }
@@ -428,7 +440,7 @@ size_t gen_lds_line(int M, int T, bool upd) {
 size_t gen_lds_col(int N, int KB) { return (size_t)2 * KB * N * 8 + (size_t)N * 8; }
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
-                        float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                        int iso, int maxit, unsigned char* ws, const Layout& lay,
                         const Traj& tr, const admm_batch_reducer* red);
 
 // the caller's cross-shard sum of an M x N map (isotropic prox over a sharded batch)
@@ -439,7 +451,7 @@ int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStr
 }
 
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
-                int kw, float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                int kw, const admm::ScalarSrc& sc, int iso, int maxit, unsigned char* ws, const Layout& lay,
                 const Traj& tr, const admm_batch_reducer* red) {
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
@@ -453,7 +465,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     float2* spec0 = reinterpret_cast<float2*>(ws + lay.spec0);
     float2* spec1 = reinterpret_cast<float2*>(ws + lay.spec1);
     const int L = M / 2;
-    const float tau = lambda / rho;   // ops.jl:20
+    float* prm = reinterpret_cast<float*>(ws + lay.prm);   // tau = lambda / rho (ops.jl:20), rho, lambda
     double2* SigT = tr.sig;
 
     rc = ln.run(ADMM_K_SETUP, [&] {
@@ -462,7 +474,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
         set_lds(admm::setup_kernel, lds);
         hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Ct, Gt, h, kh, kw, M,
-                           N, rho, SigT);
+                           N, sc, prm, SigT);
     });
     if (rc) return rc;
     if (maxit == 0) {
@@ -472,18 +484,18 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     }
 
     if (generic_shape(M, N)) {
-        return run_forward_generic(ln, y, x_out, M, N, planes, kh, lambda, rho, iso, maxit, ws, lay, tr, red);
+        return run_forward_generic(ln, y, x_out, M, N, planes, kh, iso, maxit, ws, lay, tr, red);
     }
     if (fused_shape(M, N, iso != 0) && !tr.v && fused_enabled()) {
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
         // spec0, lane-native s in sA -- or, recording a trajectory, s_k in its own slot of tr.s
         namespace pk = admm::plane;
         void* tables = ws + lay.F;
-        rc = ln.run(ADMM_K_SETUP, [&] { (void)pk::launch_tables(Ct, Gt, tables, s); });
+        rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, tables, s); });
         if (rc) return rc;
         rc = ln.run(ADMM_K_PLANE, [&] {
-            (void)pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), tau, rho, maxit,
-                                   planes, s, reinterpret_cast<float4*>(tr.s));
+            return pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
+                                   planes, s, reinterpret_cast<float4*>(tr.s), opt(ADMM_OPT_PLANE_STAGGER));
         });
         return rc;
     }
@@ -498,14 +510,14 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     const size_t np = planes;
     const dim3 gl(N / T, (unsigned)np), gc(L / KB, (unsigned)np);
     // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
-    rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
+    rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
     if (rc) return rc;
     const float2* first = spec0;
     float cs1 = 1.0f;
     if (kh > 0) {
-        rc = ln.run(ADMM_K_PREP, [&] { launch_column(N, 1, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f); });
+        rc = ln.run(ADMM_K_PREP, [&] { return launch_column(N, 1, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f); });
         if (rc) return rc;
-        rc = ln.run(ADMM_K_PREP, [&] { launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
+        rc = ln.run(ADMM_K_PREP, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
         if (rc) return rc;
         first = spec1;          // = F_dim1(H^T y) / M
         cs1 = (float)M;
@@ -514,7 +526,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     for (int it = 1; it <= maxit; ++it) {
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * np * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            launch_column(N, vsave ? 3 : 0, gc, clds, s, it == 1 ? first : spec0, spec1, Ct, Gt, twN, L, KB,
+            return launch_column(N, vsave ? 3 : 0, gc, clds, s, it == 1 ? first : spec0, spec1, Ct, Gt, twN, L, KB,
                           it == 1 ? cs1 : 1.0f, vsave);
         });
         if (rc) return rc;
@@ -529,7 +541,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 sn = (it & 1) ? sbuf[0] : sbuf[1];
             }
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, hty, twM, N, tau, rho,
+                return launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, hty, twM, N, prm,
                             it == 1 ? 1 : 0);
             });
         } else if (it < maxit) {
@@ -544,7 +556,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
             float* nrm_out = tr.nrm ? tr.nrm + (size_t)(it - 1) * MN : nullptr;
             const int ng = iso_ngroups(np);
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, so, sn, fmap, part, twM, N, (int)np,
+                return launch_iso_a(L, T, dim3(N / T, ng), iso_a_lds(M, T), s, spec1, so, sn, fmap, part, twM, N, (int)np,
                              iso_group(np), it == 1 ? 1 : 0);
             });
             if (rc) return rc;
@@ -559,19 +571,19 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 rc = call_reducer(red, fmap, MN, s);
                 if (rc) return rc;
                 rc = ln.run(ADMM_K_NORM, [&] {
-                    hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, nrm_out);
+                    hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, prm, nrm_out);
                 });
             } else {
                 rc = ln.run(ADMM_K_NORM, [&] {
-                    hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, nrm_out);
+                    hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, prm, nrm_out);
                 });
             }
             if (rc) return rc;
             rc = ln.run(ADMM_K_LINE, [&] {
-                launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, hty, spec0, twM, N, rho);
+                return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, hty, spec0, twM, N, prm);
             });
         } else {
-            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
         }
         if (rc) return rc;
     }
@@ -579,7 +591,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
 }
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
-                        float lambda, float rho, int iso, int maxit, unsigned char* ws, const Layout& lay,
+                        int iso, int maxit, unsigned char* ws, const Layout& lay,
                         const Traj& tr, const admm_batch_reducer* red) {
     namespace g = admm::gen;
     hipStream_t s = ln.s;
@@ -597,7 +609,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     float* xg = reinterpret_cast<float*>(ws + lay.xg);
     float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
-    const float tau = lambda / rho;
+    const float* prm = reinterpret_cast<const float*>(ws + lay.prm);
     const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
     const int T = gen_T(M, N), KB = gen_KB(M, N);
     const dim3 gl(N / T, (unsigned)planes), gc((H + KB - 1) / KB, (unsigned)planes);
@@ -648,8 +660,8 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
                 sn = tr.s + (size_t)(it - 1) * sstride;
             }
             rc = ln.run(ADMM_K_LINE, [&] {
-                hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, tau,
-                                   rho, it == 1 ? 1 : 0);
+                hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, prm,
+                                   it == 1 ? 1 : 0);
             });
             if (rc) return rc;
             continue;
@@ -676,26 +688,25 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             rc = call_reducer(red, fmap, MN, s);
             if (rc) return rc;
             rc = ln.run(ADMM_K_NORM, [&] {
-                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, tau, nrm_out);
+                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, prm, nrm_out);
             });
         } else {
             rc = ln.run(ADMM_K_NORM, [&] {
-                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, tau, nrm_out);
+                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, part, fmap, ng, MN, prm, nrm_out);
             });
         }
         if (rc) return rc;
         rc = ln.run(ADMM_K_LINE, [&] {
-            hipLaunchKernelGGL(g::iso_b_kernel, gl, dim3(256), lup, s, sa, fmap, hty, spec0, twM, pM, N, T, rho);
+            hipLaunchKernelGGL(g::iso_b_kernel, gl, dim3(256), lup, s, sa, fmap, hty, spec0, twM, pM, N, T, prm);
         });
         if (rc) return rc;
     }
     return ADMM_OK;
 }
 
-int check_common(const float* y, float* x, int maxit, float lambda, float rho) {
+int check_common(const float* y, float* x, int maxit) {
     if (!y || !x) return fail(ADMM_E_INVALID, "y and x_out must be device pointers");
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
-    if (!std::isfinite(lambda) || !std::isfinite(rho)) return fail(ADMM_E_INVALID, "lambda and rho must be finite");
     if ((reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(x) & 15))
         return fail(ADMM_E_INVALID, "y and x_out must be 16-byte aligned");
     return ADMM_OK;
@@ -788,13 +799,13 @@ void launch_reduce_cols(hipStream_t s, const double* part, double* out, int n, i
 
 int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
                     const float* sk, const float* xK, const float* sb_in, float* sb_out, float* vsum, float2* spec0,
-                    double* part, const float2* twM, int N, float tau, float rho, int first_k, int last_k, bool ln) {
+                    double* part, const float2* twM, int N, const float* prm, int first_k, int last_k, bool ln) {
     if (ln) {   // trajectory in the fused kernel's lane-native layout (M = 256)
 #define X(l, t)                                                                                                \
         if (L == l && T == t) {                                                                                \
             set_lds(line_adj_kernel<l, t, true>, lds);                                                         \
             line_adj_kernel<l, t, true><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, \
-                                                                  part, twM, N, tau, rho, first_k, last_k);    \
+                                                                  part, twM, N, prm, first_k, last_k);    \
             return 0;                                                                                          \
         }
         X(128, 2) X(128, 4) X(128, 8) X(128, 16)
@@ -805,7 +816,7 @@ int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
     if (L == l && T == t) {                                                                                    \
         set_lds(line_adj_kernel<l, t>, lds);                                                                   \
         line_adj_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, part, twM, \
-                                                        N, tau, rho, first_k, last_k);                        \
+                                                        N, prm, first_k, last_k);                        \
         return 0;                                                                                              \
     }
     ADMM_LT_CASES(X)
@@ -815,13 +826,13 @@ int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
 
 int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
                      const float* sk, const float* xK, const float* nrm1, const float* sb_in, float* wbar, float* vsum,
-                     float* rpartial, double* part, const float2* twM, int N, int planes, int G, float tau, float rho,
+                     float* rpartial, double* part, const float2* twM, int N, int planes, int G, const float* prm,
                      int first_k, int last_k) {
 #define X(l, t)                                                                                                 \
     if (L == l && T == t) {                                                                                     \
         set_lds(iso_adj_a_kernel<l, t>, lds);                                                                   \
         iso_adj_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, nrm1, nullptr, sb_in, wbar, vsum,  \
-                                                         rpartial, part, twM, N, planes, G, tau, rho, first_k,  \
+                                                         rpartial, part, twM, N, planes, G, prm, first_k,  \
                                                          last_k);                                               \
         return 0;                                                                                               \
     }
@@ -832,12 +843,12 @@ int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const floa
 
 int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* wbar, const float* sb_in,
                      const float* sk1, const float* nrm1, const float* Rmap, float* sb_out, float2* spec0,
-                     const float2* twM, int N, float tau, float rho) {
+                     const float2* twM, int N, const float* prm) {
 #define X(l, t)                                                                                                 \
     if (L == l && T == t) {                                                                                     \
         set_lds(iso_adj_b_kernel<l, t>, lds);                                                                   \
         iso_adj_b_kernel<l, t><<<g, kThreads, lds, s>>>(wbar, sb_in, sk1, nrm1, Rmap, sb_out, spec0, twM, N,    \
-                                                         tau, rho);                                             \
+                                                         prm);                                                  \
         return 0;                                                                                               \
     }
     ADMM_LT_CASES(X)
@@ -845,68 +856,72 @@ int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const floa
     return -1;
 }
 
-}  // namespace
 
-extern "C" {
+// ---- recordings: the path a forward-with-trajectory took, checked by its replay ----------------
+// A recording lives in the caller's workspace; its replay must run the reverse sweep that matches the
+// trajectory's layout (lane-native for the fused kernel, natural for the 2-pass and runtime-length
+// paths) and the tile choices the workspace layout was sized with.  The host keeps one tag per
+// recorded workspace; a replay whose arguments or library options differ from the recording's, or
+// whose workspace holds no recording, fails with ADMM_E_INVALID instead of reading a foreign layout.
+struct RecTag {
+    int M, N, P, B, kh, kw, iso, maxit, want_h;
+    int opts[ADMM_OPT_COUNT];
+    bool operator==(const RecTag& o) const { return std::memcmp(this, &o, sizeof(RecTag)) == 0; }
+};
+std::mutex g_rec_mu;
+std::unordered_map<const void*, RecTag> g_rec;
 
-int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
-                         float lambda, float rho, int iso, int maxit, void* workspace, size_t workspace_bytes,
-                         void* stream) {
-    return admm_tvd_forward_sharded_f32(y, x_out, M, N, P, B, h, kh, kw, lambda, rho, iso, maxit, workspace,
-                                        workspace_bytes, stream, nullptr);
+RecTag make_tag(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, bool want_h) {
+    RecTag t;
+    std::memset(&t, 0, sizeof(t));
+    t.M = M, t.N = N, t.P = P, t.B = B, t.kh = kh, t.kw = kw, t.iso = iso != 0, t.maxit = maxit, t.want_h = want_h;
+    for (int i = 0; i < ADMM_OPT_COUNT; ++i) t.opts[i] = opt(i);
+    return t;
+}
+void rec_forget(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_rec_mu);
+    g_rec.erase(ws);
 }
 
-int admm_tvd_forward_sharded_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
-                                 int kw, float lambda, float rho, int iso, int maxit, void* workspace,
-                                 size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+int check_lam_rho(float lambda, float rho) {
+    if (!std::isfinite(lambda) || !std::isfinite(rho)) return fail(ADMM_E_INVALID, "lambda and rho must be finite");
+    return ADMM_OK;
+}
+
+int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
+                 const admm::ScalarSrc& sc, int iso, int maxit, void* workspace, size_t workspace_bytes, void* stream,
+                 const admm_batch_reducer* reducer) {
     const admm_batch_reducer* red = (iso && reducer && reducer->fn) ? reducer : nullptr;
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    rc = check_common(y, x_out, maxit, lambda, rho);
+    rc = check_common(y, x_out, maxit);
     if (rc) return rc;
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
     const Layout lay = make_layout(M, N, planes, kh > 0, iso != 0);
     rc = check_ws(workspace, workspace_bytes, lay.total);
     if (rc) return rc;
+    rec_forget(workspace);   // whatever was recorded there is overwritten now
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
-    rc = run_forward(ln, y, x_out, M, N, planes, h, kh, kw, lambda, rho, iso, maxit,
-                     static_cast<unsigned char*>(workspace), lay, Traj{}, red);
+    rc = run_forward(ln, y, x_out, M, N, planes, h, kh, kw, sc, iso, maxit, static_cast<unsigned char*>(workspace), lay,
+                     Traj{}, red);
     int rc2 = ln.finish();
     return rc ? rc : rc2;
-}
-
-int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, int want_hbar,
-                                      size_t* out_bytes) {
-    if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
-    int rc = check_shape(M, N, P, B, kh, kw, iso);
-    if (rc) return rc;
-    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
-    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
-    return ADMM_OK;
-}
-
-int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
-                          float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw, float lambda,
-                          float rho, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
-                          void* stream) {
-    return admm_tvd_backward_sharded_f32(y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda,
-                                         rho, iso, maxit, x_out, workspace, workspace_bytes, stream, nullptr);
 }
 
 // phases: 1 = forward recording the trajectory into the workspace (writes x_out), 2 = reverse sweep
 // from a recorded workspace (x_out = that forward's output), 3 = both.  want_hbar_rec: phase 1 alone
 // records the extra h_bar trajectory only when asked (phase 2 must then be given h_bar).
-static int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_bar, float* y_bar, float* h_bar,
-                        float* lambda_bar, float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
-                        float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
-                        size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                 float* lambda_bar, float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                 const admm::ScalarSrc& sc, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
+                 void* stream, const admm_batch_reducer* reducer) {
     const admm_batch_reducer* red = (iso && reducer && reducer->fn) ? reducer : nullptr;
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    rc = check_common(y, (phases & 2) ? y_bar : x_out, maxit, lambda, rho);
+    rc = check_common(y, (phases & 2) ? y_bar : x_out, maxit);
     if (rc) return rc;
     if ((phases & 2) && (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)))
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
@@ -918,6 +933,22 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
+    const RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h);
+    if (phases == 2) {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        auto it = g_rec.find(workspace);
+        if (it == g_rec.end())
+            return fail(ADMM_E_INVALID, "workspace holds no recording (admm_tvd_forward_record_* first; a plain forward "
+                                        "on the same workspace overwrites it)");
+        if (!(it->second == tag))
+            return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request or "
+                                        "library options changed between record and replay)");
+        g_rec.erase(it);
+    } else {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        if (phases == 1) g_rec[workspace] = tag;
+        else g_rec.erase(workspace);
+    }
     unsigned char* ws = static_cast<unsigned char*>(workspace);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     Launcher ln{s, g_prof.on, {}};
@@ -926,7 +957,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     const bool gen = generic_shape(M, N);   // runtime-length path (admm_generic.hip, admm_generic_bwd.hip)
     const int T = gen ? gen_T(M, N) : bwd_line_T(M, N, iso != 0);
     const int KB = gen ? gen_KB(M, N) : column_KB(M, N);
-    const float tau = lambda / rho;
+    float* prm = reinterpret_cast<float*>(ws + bl.f.prm);
     const int K = maxit;
     if (!x_out || (reinterpret_cast<uintptr_t>(x_out) & 15))
         return fail(ADMM_E_INVALID, "x_out (forward output of the recomputed solve) must be a 16-byte aligned device pointer");
@@ -954,10 +985,15 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
     if (phases & 1) {
-        rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, lambda, rho, iso, K, ws, bl.f, tr, red);
+        rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, sc, iso, K, ws, bl.f, tr, red);
         if (rc) return rc;
     }
     if (!(phases & 2)) return ln.finish();
+    if (!(phases & 1)) {
+        // replay: resolve lambda / rho again from the caller's sources (the forward's values)
+        rc = ln.run(ADMM_K_SETUP, [&] { hipLaunchKernelGGL(admm::scal_kernel, dim3(1), dim3(64), 0, s, sc, prm); });
+        if (rc) return rc;
+    }
     // ---- reverse sweep ----
     float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
     float2* twN = reinterpret_cast<float2*>(ws + bl.f.twN);
@@ -980,11 +1016,11 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         namespace pk = admm::plane;
         float4* dxK = reinterpret_cast<float4*>(sb[1]);
         float* vout = kh > 0 ? vsum : y_bar;
-        rc = ln.run(ADMM_K_PREP, [&] { (void)pk::launch_dx_lane(xK, dxK, planes, s); });
+        rc = ln.run(ADMM_K_PREP, [&] { return pk::launch_dx_lane(xK, dxK, planes, s); });
         if (rc) return rc;
         rc = ln.run(ADMM_K_ADJ, [&] {
-            (void)pk::launch_plane_adj(x_bar, ws + bl.f.F, reinterpret_cast<const float4*>(tr.s), dxK,
-                                       reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, tau, rho, K, planes, s);
+            return pk::launch_plane_adj(x_bar, ws + bl.f.F, reinterpret_cast<const float4*>(tr.s), dxK,
+                                       reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s);
         });
         if (rc) return rc;
         red_rows = (int)planes;
@@ -1032,7 +1068,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             if (!iso) {
                 rc = ln.run(ADMM_K_ADJ, [&] {
                     hipLaunchKernelGGL(g::line_adj_kernel, ggl, dim3(256), lup, s, vb, sk1, skk, xK, sbi, sbo, vsum, specA,
-                                       rp, twM, pM, N, T, tau, rho);
+                                       rp, twM, pM, N, T, prm);
                 });
                 if (rc) return rc;
                 continue;
@@ -1041,13 +1077,13 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             rc = ln.run(ADMM_K_ADJ, [&] {
                 hipLaunchKernelGGL(g::iso_adj_a_kernel, dim3(N / T, (unsigned)ngi), dim3(256), (size_t)T * M * 4, s, vb,
                                    sk1, skk, xK, nrm1, sbi, wbar, vsum, Rpart, rp, M, N, (int)planes, iso_group(planes),
-                                   T, tau, rho);
+                                   T, prm);
             });
             if (rc) return rc;
             if (k == 1) break;
             rc = ln.run(ADMM_K_NORM, [&] {
                 hipLaunchKernelGGL(admm::iso_adj_r_kernel, dim3(kIsoAdjRBlocks), dim3(kThreads), 0, s, Rpart, Rmap,
-                                   nrm1, ngi, MN, tau, rp + (size_t)bl.nblk_isoA * 2);
+                                   nrm1, ngi, MN, prm, rp + (size_t)bl.nblk_isoA * 2);
             });
             if (rc) return rc;
             if (red) {
@@ -1056,18 +1092,18 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             }
             rc = ln.run(ADMM_K_ADJ, [&] {
                 hipLaunchKernelGGL(g::iso_adj_b_kernel, ggl, dim3(256), lup, s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA,
-                                   twM, pM, N, T, tau, rho);
+                                   twM, pM, N, T, prm);
             });
             if (rc) return rc;
         }
     } else if (!fused_adj) {
-        rc = ln.run(ADMM_K_PREP, [&] { launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
+        rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
         if (rc) return rc;
     }
     for (int k = (fused_adj || gen) ? 0 : K; k >= 1; --k) {
         float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
+            return launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
         });
         if (rc) return rc;
         const float* sk1 = k >= 2 ? tr.s + (size_t)(k - 2) * sstride : nullptr;
@@ -1077,7 +1113,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
         if (!iso) {
             rc = ln.run(ADMM_K_ADJ, [&] {
-                launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, tau, rho,
+                return launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, prm,
                                 k == 1 ? 1 : 0, k == K ? 1 : 0, ln_traj);
             });
             if (rc) return rc;
@@ -1086,15 +1122,15 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
         // isotropic: ISO_ADJ_A (plane groups) -> ISO_ADJ_R (batch R map, tau_bar) -> ISO_ADJ_B (per plane)
         const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
         rc = ln.run(ADMM_K_ADJ, [&] {
-            launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
-                             nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, iso_group(planes), tau, rho,
+            return launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
+                             nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, iso_group(planes), prm,
                              k == 1 ? 1 : 0, k == K ? 1 : 0);
         });
         if (rc) return rc;
         if (k == 1) break;
         rc = ln.run(ADMM_K_NORM, [&] {
             hipLaunchKernelGGL(admm::iso_adj_r_kernel, dim3(kIsoAdjRBlocks), dim3(kThreads), 0, s, Rpart, Rmap, nrm1,
-                               ngi, MN, tau, rp + (size_t)bl.nblk_isoA * 2);
+                               ngi, MN, prm, rp + (size_t)bl.nblk_isoA * 2);
         });
         if (rc) return rc;
         // sharded batch: tau_bar above used this shard's R (shard contributions add up, like every other
@@ -1104,7 +1140,7 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             if (rc) return rc;
         }
         rc = ln.run(ADMM_K_ADJ, [&] {
-            launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, tau, rho);
+            return launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, prm);
         });
         if (rc) return rc;
     }
@@ -1134,11 +1170,11 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
             rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_inv_kernel, ggl, dim3(256), lfw, s, specB, y_bar, twM, pM, N, T); });
             if (rc) return rc;
         } else {
-            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
             if (rc) return rc;
-            rc = ln.run(ADMM_K_FINAL, [&] { launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
             if (rc) return rc;
-            rc = ln.run(ADMM_K_FINAL, [&] { launch_line_inv(L, T, gl, flds, s, specB, y_bar, twM, N); });
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, specB, y_bar, twM, N); });
             if (rc) return rc;
         }
         if (h_bar) {
@@ -1173,34 +1209,132 @@ static int run_backward(int phases, int want_hbar_rec, const float* y, const flo
     rc = ln.run(ADMM_K_FINAL, [&] {
         const int nt = kh * kw > 1 ? kh * kw : 1;
         hipLaunchKernelGGL(admm::grads_final_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, rt, hcorr, hA, kh * kw,
-                           lambda, rho, lambda_bar, rho_bar, (h_bar && kh > 0) ? h_bar : nullptr);
+                           prm, lambda_bar, rho_bar, (h_bar && kh > 0) ? h_bar : nullptr);
     });
     if (rc) return rc;
 #undef HIPCHK
     return ln.finish();
 }
 
+}  // namespace
+
+extern "C" {
+
+int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
+                         float lambda, float rho, int iso, int maxit, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    return admm_tvd_forward_sharded_f32(y, x_out, M, N, P, B, h, kh, kw, lambda, rho, iso, maxit, workspace,
+                                        workspace_bytes, stream, nullptr);
+}
+
+int admm_tvd_forward_sharded_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
+                                 int kw, float lambda, float rho, int iso, int maxit, void* workspace,
+                                 size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    int rc = check_lam_rho(lambda, rho);
+    if (rc) return rc;
+    return forward_impl(y, x_out, M, N, P, B, h, kh, kw, admm::ScalarSrc{nullptr, nullptr, lambda, rho}, iso, maxit,
+                        workspace, workspace_bytes, stream, reducer);
+}
+
+int admm_tvd_forward_dev_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
+                             const float* lambda, const float* rho, int iso, int maxit, void* workspace,
+                             size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    if (!lambda || !rho) return fail(ADMM_E_INVALID, "lambda and rho must be device pointers");
+    return forward_impl(y, x_out, M, N, P, B, h, kh, kw, admm::ScalarSrc{lambda, rho, 0.f, 0.f}, iso, maxit,
+                        workspace, workspace_bytes, stream, reducer);
+}
+
+int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, int want_hbar,
+                                      size_t* out_bytes) {
+    if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
+    int rc = check_shape(M, N, P, B, kh, kw, iso);
+    if (rc) return rc;
+    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
+    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
+    return ADMM_OK;
+}
+
+int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                          float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw, float lambda,
+                          float rho, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
+                          void* stream) {
+    return admm_tvd_backward_sharded_f32(y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda,
+                                         rho, iso, maxit, x_out, workspace, workspace_bytes, stream, nullptr);
+}
+
 int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
                                   float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
                                   float lambda, float rho, int iso, int maxit, float* x_out, void* workspace,
                                   size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
-    return run_backward(3, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda, rho, iso,
-                        maxit, x_out, workspace, workspace_bytes, stream, reducer);
+    int rc = check_lam_rho(lambda, rho);
+    if (rc) return rc;
+    return run_backward(3, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{nullptr, nullptr, lambda, rho}, iso, maxit, x_out, workspace, workspace_bytes,
+                        stream, reducer);
+}
+
+int admm_tvd_backward_dev_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
+                              float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
+                              const float* lambda, const float* rho, int iso, int maxit, float* x_out, void* workspace,
+                              size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
+    if (!lambda || !rho) return fail(ADMM_E_INVALID, "lambda and rho must be device pointers");
+    return run_backward(3, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{lambda, rho, 0.f, 0.f}, iso, maxit, x_out, workspace, workspace_bytes, stream,
+                        reducer);
 }
 
 int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
                                 int kw, float lambda, float rho, int iso, int maxit, int want_hbar, void* workspace,
                                 size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
-    return run_backward(1, want_hbar, y, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, P, B, h, kh, kw, lambda,
-                        rho, iso, maxit, x_out, workspace, workspace_bytes, stream, reducer);
+    int rc = check_lam_rho(lambda, rho);
+    if (rc) return rc;
+    return run_backward(1, want_hbar, y, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{nullptr, nullptr, lambda, rho}, iso, maxit, x_out, workspace, workspace_bytes,
+                        stream, reducer);
+}
+
+int admm_tvd_forward_record_dev_f32(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh,
+                                    int kw, const float* lambda, const float* rho, int iso, int maxit, int want_hbar,
+                                    void* workspace, size_t workspace_bytes, void* stream,
+                                    const admm_batch_reducer* reducer) {
+    if (!lambda || !rho) return fail(ADMM_E_INVALID, "lambda and rho must be device pointers");
+    return run_backward(1, want_hbar, y, nullptr, nullptr, nullptr, nullptr, nullptr, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{lambda, rho, 0.f, 0.f}, iso, maxit, x_out, workspace, workspace_bytes, stream,
+                        reducer);
 }
 
 int admm_tvd_backward_recorded_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
                                    float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
                                    float lambda, float rho, int iso, int maxit, const float* x_out, void* workspace,
                                    size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer) {
-    return run_backward(2, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw, lambda, rho, iso,
-                        maxit, const_cast<float*>(x_out), workspace, workspace_bytes, stream, reducer);
+    int rc = check_lam_rho(lambda, rho);
+    if (rc) return rc;
+    return run_backward(2, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{nullptr, nullptr, lambda, rho}, iso, maxit, const_cast<float*>(x_out),
+                        workspace, workspace_bytes, stream, reducer);
+}
+
+int admm_tvd_backward_recorded_dev_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                                       float* lambda_bar, float* rho_bar, int M, int N, int P, int B, const float* h,
+                                       int kh, int kw, const float* lambda, const float* rho, int iso, int maxit,
+                                       const float* x_out, void* workspace, size_t workspace_bytes, void* stream,
+                                       const admm_batch_reducer* reducer) {
+    if (!lambda || !rho) return fail(ADMM_E_INVALID, "lambda and rho must be device pointers");
+    return run_backward(2, 0, y, x_bar, y_bar, h_bar, lambda_bar, rho_bar, M, N, P, B, h, kh, kw,
+                        admm::ScalarSrc{lambda, rho, 0.f, 0.f}, iso, maxit, const_cast<float*>(x_out), workspace,
+                        workspace_bytes, stream, reducer);
+}
+
+int admm_set_option(int option, int value) {
+    if (option < 0 || option >= ADMM_OPT_COUNT) return fail(ADMM_E_INVALID, "unknown option %d", option);
+    g_opt[option].store(value, std::memory_order_relaxed);
+    return ADMM_OK;
+}
+
+int admm_get_option(int option, int* value) {
+    if (option < 0 || option >= ADMM_OPT_COUNT || !value) return fail(ADMM_E_INVALID, "bad option query %d", option);
+    *value = opt(option);
+    return ADMM_OK;
 }
 
 int admm_profile_enable(int on) {

@@ -63,7 +63,8 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
                                                        const float* __restrict__ sb_in, float* __restrict__ sb_out,
                                                        float* __restrict__ vsum, float2* __restrict__ spec,
                                                        double* __restrict__ part, const float2* __restrict__ twM,
-                                                       FPlan pM, int N, int T, float tau, float rho) {
+                                                       FPlan pM, int N, int T, const float* __restrict__ prm) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
@@ -143,7 +144,8 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
                                                         const float* __restrict__ nrm1, const float* __restrict__ sb_in,
                                                         float* __restrict__ vbar_out, float* __restrict__ vsum,
                                                         float* __restrict__ rpartial, double* __restrict__ part,
-                                                        int M, int N, int planes, int G, int T, float tau, float rho) {
+                                                        int M, int N, int planes, int G, int T, const float* __restrict__ prm) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float* acc = reinterpret_cast<float*>(smem_raw);
     const size_t MN = (size_t)M * N;
@@ -197,7 +199,8 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
                                                         const float* __restrict__ sk1, const float* __restrict__ nrm1,
                                                         const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                         float2* __restrict__ spec, const float2* __restrict__ twM,
-                                                        FPlan pM, int N, int T, float tau, float rho) {
+                                                        FPlan pM, int N, int T, const float* __restrict__ prm) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;

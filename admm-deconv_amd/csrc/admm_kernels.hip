@@ -58,10 +58,36 @@ __device__ __forceinline__ XBlk xcd_block() {
 //   Ct[kj][k] = 1/(MN) / (|Sigma|^2 + rho(|Lx|^2 + |Ly|^2))     k = 0..M/2  (transposed: k fastest)
 //   Gt[kj][k] = 1/(MN) * conj(Sigma_centred)                      (only with a PSF)
 // ----------------------------------------------------------------------------------------------
+// Where the solve's lambda and rho come from: device pointers (the reference's 1-element CuArrays,
+// `tvd_fft(y, λ::CGPUArray, ρ::CGPUArray, ...)`, ops.jl:99,181 -- read on the device, no host sync)
+// or, when a pointer is NULL, the host value.  setup_kernel / scal_kernel resolve them once into the
+// workspace's scalar block prm = {tau = lambda / rho (fp32, ops.jl:20), rho, lambda}; every later
+// kernel of the solve reads prm.
+struct ScalarSrc {
+    const float* lam;
+    const float* rho;
+    float lam_v;
+    float rho_v;
+};
+__device__ __forceinline__ float src_lam(const ScalarSrc& sc) { return sc.lam ? *sc.lam : sc.lam_v; }
+__device__ __forceinline__ float src_rho(const ScalarSrc& sc) { return sc.rho ? *sc.rho : sc.rho_v; }
+__device__ __forceinline__ void write_prm(const ScalarSrc& sc, float* prm) {
+    const float lam = src_lam(sc), rho = src_rho(sc);
+    prm[0] = lam / rho;
+    prm[1] = rho;
+    prm[2] = lam;
+}
+__global__ void scal_kernel(ScalarSrc sc, float* __restrict__ prm) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) write_prm(sc, prm);
+}
+
 __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ twM, float2* __restrict__ twN,
                                                          float* __restrict__ Ct, float2* __restrict__ Gt,
                                                          const float* __restrict__ h, int kh, int kw, int M,
-                                                         int N, float rho, double2* __restrict__ SigT) {
+                                                         int N, ScalarSrc sc, float* __restrict__ prm,
+                                                         double2* __restrict__ SigT) {
+    const float rho = src_rho(sc);
+    if (blockIdx.x == 0 && threadIdx.x == 0) write_prm(sc, prm);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     double2* tM = reinterpret_cast<double2*>(smem_raw);  // exp(-2 pi i t / M)
     double2* tN = tM + M;                                // exp(-2 pi i t / N)
@@ -439,8 +465,9 @@ template <int L, int T>
 __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict__ spec1, float2* __restrict__ spec0,
                                                         const float* __restrict__ s_old, float* __restrict__ s_new,
                                                         const float* __restrict__ hty,
-                                                        const float2* __restrict__ twM, int N, float tau, float rho,
+                                                        const float2* __restrict__ twM, int N, const float* __restrict__ prm,
                                                         int s_zero) {
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -753,7 +780,8 @@ __device__ __forceinline__ float group_sum(const float* __restrict__ part, int n
 }
 
 __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
-                                                         int ngroups, size_t MN, float tau, float* __restrict__ nrm_out) {
+                                                         int ngroups, size_t MN, const float* __restrict__ prm, float* __restrict__ nrm_out) {
+    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
     __shared__ float red[kThreads];
     for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
         const size_t q = base + (threadIdx.x & 63);
@@ -778,8 +806,9 @@ __global__ __launch_bounds__(kThreads) void iso_sum_kernel(const float* __restri
     }
 }
 
-__global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ fmap, size_t MN, float tau,
+__global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ fmap, size_t MN, const float* __restrict__ prm,
                                                            float* __restrict__ nrm_out) {
+    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
         const float nrm = sqrtf(fmap[q]);   // fmap holds the all-reduced sum of squares
         fmap[q] = max0_nan(1.0f - tau / nrm);
@@ -790,7 +819,8 @@ __global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ f
 template <int L, int T>
 __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict__ s_new, const float* __restrict__ fmap,
                                                          const float* __restrict__ hty, float2* __restrict__ spec0,
-                                                         const float2* __restrict__ twM, int N, float rho) {
+                                                         const float2* __restrict__ twM, int N, const float* __restrict__ prm) {
+    const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;

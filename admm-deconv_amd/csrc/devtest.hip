@@ -40,11 +40,15 @@ template <int MODE, bool PSF = false>
 int plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,
                        float rho, int K, int planes, float* dbg, const float* Gf = nullptr, const float* G0b = nullptr) {
     namespace pk = admm::plane;
+    static float* prm = nullptr;   // the kernel reads {tau, rho} from device memory (setup_kernel's block)
+    if (!prm && hipMalloc(&prm, 16) != hipSuccess) return -4;
+    const float hp[4] = {tau, rho, 0.f, 0.f};
+    if (hipMemcpy(prm, hp, sizeof(hp), hipMemcpyHostToDevice) != hipSuccess) return -4;
     (void)hipFuncSetAttribute((const void*)pk::plane256_kernel<PSF, MODE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)pk::kLdsBytes);
     hipLaunchKernelGGL((pk::plane256_kernel<PSF, MODE>), dim3(planes), dim3(pk::kPT), pk::kLdsBytes, 0, y, x, Cf, C0b,
                        reinterpret_cast<const float2*>(Gf), reinterpret_cast<const float2*>(G0b),
-                       reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), tau, rho, K,
+                       reinterpret_cast<float2*>(hln), reinterpret_cast<float4*>(sln), prm, K,
                        reinterpret_cast<float2*>(dbg), 0);
     return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
 }

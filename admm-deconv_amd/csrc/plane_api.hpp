@@ -26,8 +26,11 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 // traj != NULL: record s_1..s_{K-1} for the adjoint, slot k-1 at traj + (k-1) * planes * 64 * 512
 // (lane-native: float4 (s0[p], s0[p+1], s1[p], s1[p+1]) of pixel pair p = 4n + 2h of line r at
 // [plane][n][2r + h]; s0 = x - x(line r-1), s1 = x - x(pixel p-1)); sln is then unused
+// prm: device {tau, rho, lambda} (setup_kernel); stagger: experiment option ADMM_OPT_PLANE_STAGGER (realtime
+// ticks of 10 ns that odd workgroups start late; 0 = off)
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        float tau, float rho, int K, size_t planes, hipStream_t s, float4* traj = nullptr);
+                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj = nullptr,
+                        int stagger = 0);
 
 
 // Reverse sweep of the anisotropic solve on the fused trajectory (plane256_adj_kernel):
@@ -37,7 +40,7 @@ hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool p
 // part: 2 doubles per plane (rho_bar, tau_bar partial sums, fixed summation order).
 hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s);
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
-                            float2* vsl, float* vout, double* part, float tau, float rho, int K, size_t planes,
+                            float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
                             hipStream_t s);
 
 }  // namespace plane

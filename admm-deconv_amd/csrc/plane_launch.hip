@@ -1,7 +1,5 @@
 // plane_launch.hip -- translation unit of the fused per-plane kernel (built without packed FP32,
 // see plane_api.hpp) and its host launchers.
-#include <cstdlib>
-
 #include "plane_api.hpp"
 #include "plane_kernel.hip"
 
@@ -33,28 +31,24 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 }
 
 template <bool PSF, bool TRAJ>
-static void launch_one(const float* y, float* x_out, const Tables& t, float2* hln, float4* sln, float tau, float rho,
+static void launch_one(const float* y, float* x_out, const Tables& t, float2* hln, float4* sln, const float* prm,
                        int K, size_t planes, hipStream_t s, int stagger, float4* traj) {
     (void)hipFuncSetAttribute((const void*)plane256_kernel<PSF, 0, TRAJ>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kLdsBytes);
     hipLaunchKernelGGL((plane256_kernel<PSF, 0, TRAJ>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out,
-                       t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, tau, rho, K, nullptr, stagger, traj,
+                       t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, prm, K, nullptr, stagger, traj,
                        planes * 64 * kPT);
 }
 
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        float tau, float rho, int K, size_t planes, hipStream_t s, float4* traj) {
+                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj, int stagger) {
     const Tables t = carve(tables);
-    static const int stagger = [] {
-        const char* e = getenv("ADMM_PLANE_STAGGER");   // experiment knob: realtime ticks (10 ns)
-        return e ? atoi(e) : 0;
-    }();
     if (psf) {
-        if (traj) launch_one<true, true>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
-        else launch_one<true, false>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
+        if (traj) launch_one<true, true>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
+        else launch_one<true, false>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
     } else {
-        if (traj) launch_one<false, true>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
-        else launch_one<false, false>(y, x_out, t, hln, sln, tau, rho, K, planes, s, stagger, traj);
+        if (traj) launch_one<false, true>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
+        else launch_one<false, false>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
     }
     return hipGetLastError();
 }
@@ -66,13 +60,13 @@ hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream
 }
 
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
-                            float2* vsl, float* vout, double* part, float tau, float rho, int K, size_t planes,
+                            float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
                             hipStream_t s) {
     const Tables t = carve(tables);
     (void)hipFuncSetAttribute((const void*)plane256_adj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kLdsBytes);
     hipLaunchKernelGGL(plane256_adj_kernel, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf, t.C0b, traj,
-                       planes * 64 * kPT, dxK, sbar, vsl, vout, part, tau, rho, K);
+                       planes * 64 * kPT, dxK, sbar, vsl, vout, part, prm, K);
     return hipGetLastError();
 }
 

@@ -1,10 +1,15 @@
 """Benchmark: ADMM TV-deconvolution images/s at 256x256, K=25 (BASELINE.json metric, config c2).
 
-One "step" = one full tvd_fft solve (src/ops/ops.jl:181 semantics) of a batch of 512 synthetic
+One "step" = one full tvd_fft solve (src/ops/ops.jl:181 semantics) of a batch of synthetic
 Gaussian-blurred 256x256 images (15x15 PSF, lambda 0.0041, rho 0.021, K = 25, anisotropic) that is
-already resident in HBM, through the HIP library's C ABI.  With N ranks (torchrun, one process per
-GPU) every rank solves its own 512-image shard (weak scaling, no data-path collective; --gather adds
-the RCCL gather of all outputs to rank 0 inside the timed region).
+already resident in HBM, through the HIP library's C ABI.
+
+  N = 1 (default): BASELINE c2, batch 512 on one GPU.
+  N > 1: BASELINE c3, batch 2048 sharded over the N GPUs (2048/N images per GPU, one process per GPU,
+         RCCL over xGMI) plus the RCCL gather of every output to rank 0 inside the timed region.  The
+         gather of one batch runs on its own stream and overlaps the solve of the next
+         (admm_deconv.parallel.ShardGather).  `python bench.py --gpus N` spawns the N ranks itself; the
+         driver's `torchrun --nproc-per-node N bench.py --gpus N` sets RANK/WORLD_SIZE and is used as is.
 
 Prints ONE JSON line on rank 0.  Besides the driver's keys it carries
   roofline      -- dominant kernel: algorithmic bytes per launch / measured avg launch duration
@@ -34,7 +39,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import admm_deconv  # noqa: E402
-from admm_deconv import _lib, synth  # noqa: E402
+from admm_deconv import _lib, parallel, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -66,12 +71,19 @@ def kernel_bytes_per_plane(M, N, K):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU); spawned here unless "
+                    "launched by torchrun")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(synth.CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(synth.CONFIGS),
+                    help="default: c2 on one GPU, c3 (2048 global, sharded + gathered) on N > 1")
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's; c3 -> 2048/N)")
-    ap.add_argument("--gather", action="store_true", help="RCCL gather of all outputs to rank 0 inside the timed region")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the gather to rank 0 (solve only)")
+    ap.add_argument("--chunks", type=int, default=1, help="N > 1: slices per shard, each gathered as soon as solved")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1: nccl (RCCL over xGMI); gloo only to rehearse the schedule with ranks sharing a GPU")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (admm_set_option), e.g. FUSED=0 or LINE_T=4; experiments only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic images generated per rank (tiled)")
@@ -214,37 +226,75 @@ def load_traffic(cfg_name, kernel):
         return None
 
 
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without torchrun: start N rank processes (one per GPU) before this
+    process touches the GPU, and exit with the worst of their exit codes.  Only rank 0 prints."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    sys.exit(bad[0] if bad else 0)
+
+
 def main():
     args = parse()
-    if args.config == "c5":
-        return bench_c5(args, torch.device("cuda", 0))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    for kv in args.opt:
+        k, v = kv.split("=")
+        _lib.set_option(k.strip().upper(), int(v))
+    config = args.config or ("c2" if world == 1 else "c3")
+    if config == "c5":
+        return bench_c5(args, torch.device("cuda", 0))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    cfg = dict(synth.CONFIGS[args.config])
+        if args.backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local if args.backend == "nccl" else local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
+    cfg = dict(synth.CONFIGS[config])
     if args.batch:
         B = args.batch
-    elif args.config == "c3":
+    elif config == "c3":
         B = cfg["B"] // world
     else:
         B = cfg["B"]
     M, N, P, K = cfg["M"], cfg["N"], cfg["P"], cfg["K"]
+    gather = world > 1 and not args.no_gather
     y, h, psf_np, base = make_inputs(cfg, B, g0=rank * B, distinct=args.distinct, dev=dev)
     out = torch.empty_like(y)
-    ws = admm_deconv.Workspace()
+    ws = [admm_deconv.Workspace() for _ in range(max(1, args.chunks))]
     stream = torch.cuda.current_stream(dev)
-    gathered = None
-    if args.gather and world > 1 and rank == 0:
-        gathered = [torch.empty_like(y) for _ in range(world)]
+    chunk_of = {}
+
+    def solve(ys, xs):
+        # one workspace per chunk slot (chunks of one step are enqueued back to back on one stream)
+        i = chunk_of.setdefault(ys.data_ptr(), len(chunk_of) % len(ws))
+        admm_deconv.tvd_fft(ys, synth.LAMBDA, synth.RHO, h, False, K, out=xs, workspace=ws[i], stream=stream)
+
+    sg = parallel.ShardGather(y, solve, chunks=args.chunks) if gather else None
 
     def step():
-        admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws, stream=stream)
-        if args.gather and world > 1:
-            dist.gather(out, gathered, dst=0)
+        if sg is not None:
+            sg.step()
+        else:
+            solve(y, out)
 
     for _ in range(args.warmup):
         step()
@@ -255,6 +305,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if sg is not None:
+        sg.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -272,7 +324,7 @@ def main():
     _lib.profile_enable(True)
     reps = 2
     for _ in range(reps):
-        admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws, stream=stream)
+        admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws[0], stream=stream)
     _lib.profile_enable(False)
     planes = B * P
     kb = kernel_bytes_per_plane(M, N, K)
@@ -289,7 +341,7 @@ def main():
         kernels[name] = e
     dom = max((k for k in kernels if k in kb), key=lambda k: kernels[k]["total_ms_per_solve"])
     alg_bytes = kb["plane"] * planes if "plane" in kernels else canonical_bytes(M, N, K) * planes
-    traffic = load_traffic(args.config, dom)
+    traffic = load_traffic(config, dom)
     ach = kernels[dom]["achieved_GBps"]
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -317,10 +369,12 @@ def main():
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{args.config}: batch {B}/GPU of {M}x{N}x{P}, {cfg['psf'][0]}x{cfg['psf'][0]} "
+            "config": {"workload": f"{config}: batch {B}/GPU of {M}x{N}x{P}, {cfg['psf'][0]}x{cfg['psf'][0]} "
                                    f"Gaussian PSF (sigma {cfg['psf'][1]}), K={K}, anisotropic TV, lambda {synth.LAMBDA}, "
                                    f"rho {synth.RHO}", "global_batch": B * world, "image": [M, N, P], "K": K,
-                       "parallelism": f"batch-shard x{world}" + (" + RCCL gather" if args.gather and world > 1 else "")},
+                       "parallelism": f"batch-shard x{world}" + (
+                           (" + RCCL gather" if args.backend == "nccl" else " + gloo gather") + " (overlapped, "
+                           f"{args.chunks} chunk{'s' if args.chunks > 1 else ''}/shard)" if gather else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": kernels,

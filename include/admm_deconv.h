@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 1
+#define ADMM_ABI_VERSION 2
 
 enum {
     ADMM_OK = 0,
@@ -129,9 +129,13 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
  * admm_tvd_backward_workspace_bytes with the same arguments and want_hbar), the backward later runs
  * only the reverse sweep from it -- the forward is not recomputed.  Between the two calls the
  * workspace must not be touched and x_out must still hold the recorded forward's output; y, h,
- * lambda, rho, iso, maxit and the environment (ADMM_FUSED) must be the same.  h_bar must be
+ * lambda, rho, iso, maxit and the library options (admm_set_option) must be the same.  h_bar must be
  * non-NULL in the backward iff want_hbar was set in the forward.  With a reducer (iso, sharded
- * batch) both calls must get one.  admm_tvd_backward_f32 is exactly the two calls back to back. */
+ * batch) both calls must get one.  admm_tvd_backward_f32 is exactly the two calls back to back.
+ * The library remembers, per workspace, the arguments and options a recording was made with: a replay
+ * that differs (or a workspace that holds no recording -- a plain forward on it overwrites one)
+ * fails with ADMM_E_INVALID rather than reading a trajectory of another layout.  A recording is
+ * consumed by its replay. */
 int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B,
                                 const float* h, int kh, int kw, float lambda, float rho, int iso,
                                 int maxit, int want_hbar, void* workspace, size_t workspace_bytes,
@@ -142,6 +146,50 @@ int admm_tvd_backward_recorded_f32(const float* y, const float* x_bar, float* y_
                                    int maxit, const float* x_out, void* workspace,
                                    size_t workspace_bytes, void* stream,
                                    const admm_batch_reducer* reducer);
+
+/* Device-resident λ and ρ.  The reference operator takes them as 1-element device arrays,
+ * tvd_fft(y, λ::CGPUArray, ρ::CGPUArray, h, ...) (ops.jl:99,181), and the layer clamps them on the
+ * device (deconv_admm.jl:216-217).  These entry points take `lambda` and `rho` as DEVICE pointers to
+ * one fp32 each, read in-kernel (τ = λ/ρ is formed on the device), so a training step never reads
+ * them back to the host.  Otherwise identical to the host-scalar entry points above; `reducer` may be
+ * NULL (unsharded).  The values must be finite and ρ > 0 (not checked: checking would need a host
+ * read); the reference has no guard either. */
+int admm_tvd_forward_dev_f32(const float* y, float* x_out, int M, int N, int P, int B,
+                             const float* h, int kh, int kw, const float* lambda, const float* rho,
+                             int iso, int maxit, void* workspace, size_t workspace_bytes, void* stream,
+                             const admm_batch_reducer* reducer);
+int admm_tvd_backward_dev_f32(const float* y, const float* x_bar, float* y_bar, float* h_bar,
+                              float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
+                              const float* h, int kh, int kw, const float* lambda, const float* rho,
+                              int iso, int maxit, float* x_out, void* workspace,
+                              size_t workspace_bytes, void* stream, const admm_batch_reducer* reducer);
+int admm_tvd_forward_record_dev_f32(const float* y, float* x_out, int M, int N, int P, int B,
+                                    const float* h, int kh, int kw, const float* lambda,
+                                    const float* rho, int iso, int maxit, int want_hbar,
+                                    void* workspace, size_t workspace_bytes, void* stream,
+                                    const admm_batch_reducer* reducer);
+int admm_tvd_backward_recorded_dev_f32(const float* y, const float* x_bar, float* y_bar,
+                                       float* h_bar, float* lambda_bar, float* rho_bar, int M, int N,
+                                       int P, int B, const float* h, int kh, int kw,
+                                       const float* lambda, const float* rho, int iso, int maxit,
+                                       const float* x_out, void* workspace, size_t workspace_bytes,
+                                       void* stream, const admm_batch_reducer* reducer);
+
+/* Library options: process-global switches read at each call.  The defaults are the tuned choices;
+ * the others exist for tests (fused vs 2-pass paths) and tuning experiments.  Not read from the
+ * environment.  A recording remembers the options it was made with (see above). */
+enum {
+    ADMM_OPT_FUSED = 0,          /* 1 (default): fused per-plane kernel at 256x256 anisotropic; 0: 2-pass */
+    ADMM_OPT_FUSED_ADJ = 1,      /* 1 (default): fused reverse sweep on a fused trajectory; 0: 2-pass    */
+    ADMM_OPT_LINE_T = 2,         /* 0 (default): tile policy; 2/4/8/16: cap on lines per line block      */
+    ADMM_OPT_COL_THREADS = 3,    /* 0 (default): policy; 256 or 1024 threads per column block            */
+    ADMM_OPT_GEN_TM = 4,         /* 0 (default 2048): runtime-length line block points, 256..8192        */
+    ADMM_OPT_GEN_KN = 5,         /* 0 (default 1024): runtime-length column block points, 256..8192      */
+    ADMM_OPT_PLANE_STAGGER = 6,  /* 0 (default): fused kernel odd-workgroup start delay, 10 ns ticks     */
+    ADMM_OPT_COUNT = 7
+};
+int admm_set_option(int option, int value);
+int admm_get_option(int option, int* value);
 
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises

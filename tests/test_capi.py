@@ -29,7 +29,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for name in header_functions():
         assert hasattr(L, name), name
-    assert L.admm_abi_version() == 1
+    assert L.admm_abi_version() == 2
 
 
 def test_workspace_bytes():
@@ -89,3 +89,46 @@ def test_generic_shapes_workspace(M, N):
             assert L.admm_tvd_backward_workspace_bytes(M, N, 1, 2, 5, 5, iso, 4, want_h, ctypes.byref(out)) == _lib.ADMM_OK
             # trajectory (3 slots of s) + the dim-2 spectra when h_bar is wanted
             assert out.value >= 3 * 2 * 2 * M * N * 4 + want_h * 4 * 2 * (M // 2 + 1) * N * 8
+
+
+def test_options_roundtrip_and_validation():
+    """Library behaviour is switched by admm_set_option, never by the environment."""
+    L = _lib.load()
+    assert _lib.get_option("FUSED") == 1 and _lib.get_option("FUSED_ADJ") == 1
+    with _lib.option("LINE_T", 4):
+        assert _lib.get_option("LINE_T") == 4
+    assert _lib.get_option("LINE_T") == 0
+    assert L.admm_set_option(99, 1) == _lib.ADMM_E_INVALID
+    assert L.admm_set_option(-1, 1) == _lib.ADMM_E_INVALID
+    v = ctypes.c_int(0)
+    assert L.admm_get_option(7, ctypes.byref(v)) == _lib.ADMM_E_INVALID
+    os.environ["ADMM_FUSED"] = "0"          # the round-1 environment knob is gone
+    try:
+        assert _lib.get_option("FUSED") == 1
+    finally:
+        del os.environ["ADMM_FUSED"]
+
+
+def test_device_scalar_entry_points_validate():
+    """The device-resident lambda / rho entry points (ops.jl:99,181 take 1-element device arrays) reject
+    NULL scalar pointers before any device work."""
+    L = _lib.load()
+    fake = 1 << 20
+    assert L.admm_tvd_forward_dev_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, None, fake, 0, 5, fake, 1 << 30, None,
+                                      None) == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_forward_record_dev_f32(fake, fake, 64, 64, 1, 1, None, 0, 0, fake, None, 0, 5, 0, fake,
+                                             1 << 30, None, None) == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_backward_dev_f32(fake, fake, fake, None, None, None, 64, 64, 1, 1, None, 0, 0, None, None, 0,
+                                       5, fake, fake, 1 << 30, None, None) == _lib.ADMM_E_INVALID
+    assert b"device pointers" in L.admm_last_error()
+
+
+def test_replay_without_recording_is_rejected():
+    """A reverse sweep on a workspace that holds no recording fails with ADMM_E_INVALID (host-side
+    check, before any device work)."""
+    L = _lib.load()
+    fake = 1 << 21   # 256-byte aligned, never dereferenced
+    rc = L.admm_tvd_backward_recorded_f32(fake, fake, fake, None, None, None, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0,
+                                          0, 5, fake, fake, 1 << 34, None, None)
+    assert rc == _lib.ADMM_E_INVALID
+    assert b"no recording" in L.admm_last_error()

@@ -13,7 +13,7 @@ import torch
 
 import admm_deconv
 import oracle_torch
-from admm_deconv import synth
+from admm_deconv import _lib, synth
 from parity import assert_parity
 
 pytestmark = pytest.mark.gpu
@@ -145,10 +145,10 @@ def test_backward_deterministic(dev, iso):
 
 
 @pytest.mark.parametrize("with_psf", [False, True])
-def test_backward_fused_trajectory(dev, with_psf, monkeypatch):
+def test_backward_fused_trajectory(dev, with_psf):
     """256 x 256 anisotropic without h_bar: the fused plane kernel records the trajectory (lane-native
     s slots) and the reverse sweep reads it.  Against the fp64 oracle, and against the 2-pass
-    trajectory (ADMM_FUSED=0)."""
+    trajectory (library option FUSED = 0)."""
     B, M, N, K, lam, rho = 2, 256, 256, 12, 0.0041, 0.021
     h = synth.gaussian_psf(15, 2.5) if with_psf else None
     y = synth.make_batch(B, M, N, h, g0=3)
@@ -156,8 +156,8 @@ def test_backward_fused_trajectory(dev, with_psf, monkeypatch):
     ht = None if h is None else torch.from_numpy(h).to(dev)
     yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
     x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(yt, xt, lam, rho, ht, False, K, need_h=False)
-    monkeypatch.setenv("ADMM_FUSED", "0")
-    x2, yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward(yt, xt, lam, rho, ht, False, K, need_h=False)
+    with _lib.option("FUSED", 0):
+        x2, yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward(yt, xt, lam, rho, ht, False, K, need_h=False)
     torch.cuda.synchronize()
     assert hb is None
     x0, yb0, _, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
@@ -205,10 +205,10 @@ FUSED_ADJ_CASES = [
 
 @pytest.mark.parametrize("case", FUSED_ADJ_CASES,
                          ids=[f"{c[0]}x{c[1]}-{'psf' if c[2] else 'nopsf'}-K{c[5]}" for c in FUSED_ADJ_CASES])
-def test_backward_fused_adjoint(dev, case, monkeypatch):
+def test_backward_fused_adjoint(dev, case):
     """256 x 256 anisotropic, no h_bar: the reverse sweep runs in plane256_adj_kernel (one workgroup per
     plane, all K steps).  Against the fp64 oracle, and against the 2-pass reverse sweep over the SAME
-    recorded trajectory (ADMM_FUSED_ADJ=0: same ST masks, so only fp32 rounding separates the two)."""
+    recorded trajectory (option FUSED_ADJ = 0: same ST masks, so only fp32 rounding separates the two)."""
     B, P, spec, lam, rho, K = case
     rng = np.random.default_rng(K + 17 * B)
     h = psf(spec, rng)
@@ -218,9 +218,9 @@ def test_backward_fused_adjoint(dev, case, monkeypatch):
     yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
     x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
     yb, _, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt)
-    x_, rec2 = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
-    monkeypatch.setenv("ADMM_FUSED_ADJ", "0")
-    yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward_recorded(rec2, x_, xt)
+    with _lib.option("FUSED_ADJ", 0):   # the record and its replay must see the same options
+        x_, rec2 = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
+        yb2, _, lb2, rb2 = admm_deconv.tvd_fft_backward_recorded(rec2, x_, xt)
     torch.cuda.synchronize()
     assert torch.equal(x, x_)
     yb_, yb2_ = yb.cpu().numpy(), yb2.cpu().numpy()

@@ -1,16 +1,15 @@
 """GPU parity of the fused per-plane kernel (plane_kernel.hip: 256 x 256, anisotropic prox).
 
-The fused path is the default for these shapes; ADMM_FUSED=0 forces the 2-pass path.  Both are
+The fused path is the default for these shapes; the library option FUSED = 0 forces the 2-pass path.  Both are
 checked against the fp64 oracle (oracle/oracle_np.py, /root/reference/src/ops/ops.jl:17-96) with the
 tolerance of tests/parity.py, and against each other."""
-import os
 
 import numpy as np
 import pytest
 import torch
 
 import admm_deconv
-from admm_deconv import synth
+from admm_deconv import _lib, synth
 from parity import assert_parity
 from test_gpu_parity import make_psf, run_gpu, run_oracle
 
@@ -30,16 +29,8 @@ CASES = [
 ]
 
 
-class fused_off:
-    def __enter__(self):
-        self.old = os.environ.get("ADMM_FUSED")
-        os.environ["ADMM_FUSED"] = "0"
-
-    def __exit__(self, *a):
-        if self.old is None:
-            del os.environ["ADMM_FUSED"]
-        else:
-            os.environ["ADMM_FUSED"] = self.old
+def fused_off():
+    return _lib.option("FUSED", 0)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}-{c[2][0] if c[2] else 'none'}-K{c[5]}" for c in CASES])
