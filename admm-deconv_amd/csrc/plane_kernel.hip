@@ -111,10 +111,27 @@ __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ float clip_tau(float v, float tau) { return fminf(fmaxf(v, -tau), tau); }
+// PLANE_PROX selects the form of the prox arithmetic (same values for every finite input):
+//   0: clip = min(max(v, -tau), tau); w = |s| > tau ? s - 2 tau sign(s) : -s   (compare + select)
+//   1: clip = med3(v, -tau, tau) (one v_med3_f32); w = s - 2 clip(s) as one FMA (exact: s - 2s = -s,
+//      s - 2 tau sign(s) has one rounding either way)
+#ifndef PLANE_PROX
+#define PLANE_PROX 0
+#endif
+__device__ __forceinline__ float clip_tau(float v, float tau) {
+#if PLANE_PROX == 1
+    return __builtin_amdgcn_fmed3f(v, -tau, tau);
+#else
+    return fminf(fmaxf(v, -tau), tau);
+#endif
+}
 // w = z - u with z = ST(s, tau) and u = s - z  (|s| > tau: s - 2 tau sign s, else -s)
 __device__ __forceinline__ float phi_tau(float s, float tau) {
+#if PLANE_PROX == 1
+    return fmaf(-2.0f, clip_tau(s, tau), s);
+#else
     return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s;
+#endif
 }
 
 // Lane-native spectral tables, built once per call from the 2-pass tables Ct/Gt (bin (kj, k) at

@@ -7,7 +7,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "admm-deconv_amd"))
 import admm_deconv  # noqa: E402
-from admm_deconv import synth  # noqa: E402
+from admm_deconv import _lib, synth  # noqa: E402
 
 dev = torch.device("cuda:0")
 runs = int(sys.argv[1]) if len(sys.argv) > 1 else 5
@@ -17,9 +17,9 @@ for psf in (True, False):
     ht = None if h is None else torch.from_numpy(h).to(dev)
     y = torch.from_numpy(synth.make_batch(64, 256, 256, h)).to(dev).repeat(8, 1, 1, 1).contiguous()
     for K in (3, 8):
-        os.environ["ADMM_FUSED"] = "0"
+        _lib.set_option("FUSED", int("0"))
         ref = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, K)
-        os.environ["ADMM_FUSED"] = "1"
+        _lib.set_option("FUSED", int("1"))
         first = None
         bad_ref = bad_rr = 0
         for _ in range(runs):

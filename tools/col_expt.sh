@@ -3,8 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 for nt in 256 1024; do
-  ADMM_COL_THREADS=$nt timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/col_c4_$nt.json 2>/dev/null || exit 1
-  ADMM_COL_THREADS=$nt timeout -k 10 300 python bench.py --config c5 --steps 3 --warmup 1 > gpurun_out/col_c5_$nt.json 2>/dev/null || exit 1
+  timeout -k 10 300 python bench.py --opt COL_THREADS=$nt --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/col_c4_$nt.json 2>/dev/null || exit 1
+  timeout -k 10 300 python bench.py --opt COL_THREADS=$nt --config c5 --steps 3 --warmup 1 > gpurun_out/col_c5_$nt.json 2>/dev/null || exit 1
 done
 for f in gpurun_out/col_*.json; do python - "$f" <<'PY'
 import json, sys

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 for t in 8 4 2; do
-  ADMM_LINE_T=$t timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/lt_c4_$t.json 2>/dev/null || exit 1
+  timeout -k 10 300 python bench.py --opt LINE_T=$t --config c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/lt_c4_$t.json 2>/dev/null || exit 1
 done
 for f in gpurun_out/lt_*.json; do python - "$f" <<'PY'
 import json, sys

@@ -9,7 +9,7 @@ for v in base "$@"; do
   echo "== $v"
   timeout -k 10 200 python tools/census_plane.py 2 2>&1 | tail -1 || break
   for b in 64 512; do
-    ADMM_FUSED=1 timeout -k 10 120 python tools/time_plane.py $b 2>&1 | grep "fused=1" | cut -c1-50 || break
+    timeout -k 10 120 python tools/time_plane.py $b 2>&1 | grep "fused=1" | cut -c1-50 || break
   done
 done
 cp /tmp/base_lib.so $L

@@ -12,6 +12,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import admm_deconv  # noqa: E402
 from admm_deconv import _lib, synth  # noqa: E402
 
+# NAME=VALUE arguments are library options (admm_set_option), e.g. FUSED=0 LINE_T=4 GEN_TM=4096
+for _a in [a for a in sys.argv[1:] if "=" in a]:
+    _lib.set_option(_a.split("=")[0].upper(), int(_a.split("=")[1]))
+    sys.argv.remove(_a)
+
 SHAPES = [(480, 640, 64, 25), (96, 96, 512, 25), (250, 250, 256, 25), (2048, 2048, 8, 25), (256, 256, 512, 25)]
 
 

@@ -9,6 +9,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import admm_deconv  # noqa: E402
 from admm_deconv import _lib, synth  # noqa: E402
 
+# NAME=VALUE arguments are library options (admm_set_option), e.g. FUSED=0 LINE_T=4 GEN_TM=4096
+for _a in [a for a in sys.argv[1:] if "=" in a]:
+    _lib.set_option(_a.split("=")[0].upper(), int(_a.split("=")[1]))
+    sys.argv.remove(_a)
+
 dev = torch.device("cuda:0")
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 h = synth.gaussian_psf(15, 2.5)
@@ -18,7 +23,7 @@ ht = torch.from_numpy(h).to(dev)
 ws = admm_deconv.Workspace()
 out = torch.empty_like(y)
 for mode in ("1", "0"):
-    os.environ["ADMM_FUSED"] = mode
+    _lib.set_option("FUSED", int(mode))
     for _ in range(2):
         admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 25, out=out, workspace=ws)
     torch.cuda.synchronize()

@@ -6,7 +6,7 @@ cp $L /tmp/base_lib.so
 for v in base "$@"; do
   if [ $v != base ]; then cp admm-deconv_amd/libadmm_deconv_$v.so $L; fi
   for b in ${BATCHES:-64 256 512}; do
-    echo "== $v $b"; ADMM_FUSED=1 timeout -k 10 120 python tools/time_plane.py $b 2>&1 | grep "fused=1" | cut -c1-50 || break
+    echo "== $v $b"; timeout -k 10 120 python tools/time_plane.py $b 2>&1 | grep "fused=1" | cut -c1-50 || break
   done
 done
 cp /tmp/base_lib.so $L
