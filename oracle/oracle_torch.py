@@ -69,15 +69,17 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100):
     return x
 
 
-def tvd_fft_grads(y, lam, rho, h, iso, maxit, xbar):
-    """fp64 autograd gradients of <xbar, x(y, lam, rho, h)>: returns (x, ybar, hbar, lambar, rhobar)."""
-    y = torch.as_tensor(y, dtype=torch.float64).clone().requires_grad_(True)
-    lam_t = torch.tensor(float(lam), dtype=torch.float64, requires_grad=True)
-    rho_t = torch.tensor(float(rho), dtype=torch.float64, requires_grad=True)
+def tvd_fft_grads(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64):
+    """Autograd gradients of <xbar, x(y, lam, rho, h)> in `dtype` (fp64: the gradient oracle; fp32: what an
+    fp32 implementation of the reference's own Zygote pass gets, used to size the gradient tolerances):
+    returns (x, ybar, hbar, lambar, rhobar)."""
+    y = torch.as_tensor(y, dtype=dtype).clone().requires_grad_(True)
+    lam_t = torch.tensor(float(lam), dtype=dtype, requires_grad=True)
+    rho_t = torch.tensor(float(rho), dtype=dtype, requires_grad=True)
     h_t = None
     if h is not None and h.size:
-        h_t = torch.as_tensor(h, dtype=torch.float64).clone().requires_grad_(True)
+        h_t = torch.as_tensor(h, dtype=dtype).clone().requires_grad_(True)
     x = tvd_fft_torch(y, lam_t, rho_t, h_t, iso, maxit)
-    (x * torch.as_tensor(xbar, dtype=torch.float64)).sum().backward()
+    (x * torch.as_tensor(xbar, dtype=dtype)).sum().backward()
     return (x.detach().numpy(), y.grad.numpy(), None if h_t is None else h_t.grad.numpy(),
             float(lam_t.grad) if lam_t.grad is not None else 0.0, float(rho_t.grad) if rho_t.grad is not None else 0.0)

@@ -29,6 +29,8 @@ FIXTURES = [
     ("even_psf10_64x128_k15", 2, 1, 128, 64, ("rand", 10, 10), 0.01, 0.05, False, 15),
     ("denoise_rgb_64_k30", 2, 3, 64, 64, None, 0.05, 0.02, False, 30),
     ("nonpow2_40x48_k5", 1, 1, 40, 48, ("gauss", 5, 1.0), 0.0041, 0.021, False, 5),
+    # BASELINE c4 (512^2, 15x15 PSF, K = 50): one plane of the RGB batch (planes are independent)
+    ("c4_512_k50_plane", 1, 1, 512, 512, ("gauss", 15, 2.5), 0.0041, 0.021, False, 50),
 ]
 
 

@@ -5,8 +5,16 @@ disagree on the mask of the rare elements with |s_k| within ~1e-5 of tau (2 of 2
 and each such flip perturbs the gradient locally (y_bar: one blob of radius ~40 px) and the heavily
 cancelling scalar sums (lambda_bar = tau_bar/rho) by a large absolute amount.  PyTorch's own fp32
 autograd shows the same effect.  Criteria (tolerances per case in CASES):
-  y_bar: trimmed per-plane relative L2 (worst 1% of pixels removed) <= 1e-4, full <= 1e-2;
-  lambda_bar, rho_bar, h_bar: relative error <= the case's scalar tolerance."""
+  y_bar: trimmed per-plane relative L2 (worst 1% of pixels removed) <= 1e-4, full <= 5e-3;
+  lambda_bar, rho_bar, h_bar: relative error <= the case's scalar tolerance: 1e-3, or 5e-3 where mask flips
+  occur (256^2 at K >= 25).
+How the mask-flip bound was measured (tools/grad_bounds.py, profiles/r02_grad_bounds.txt): on every case
+below, the GPU error next to the error of an fp32 autograd of the same oracle (what an fp32 run of the
+reference's own Zygote pass gets).  Where flips occur the fp32 autograd is off by up to 1.2e-2 (lambda_bar),
+1.6e-3 (rho_bar), 1.3e-3 (h_bar), 2.6e-3 (y_bar full); the GPU by at most 1.8e-3, 1.1e-3, 1.8e-4, 3.7e-4.
+5e-3 sits above the GPU's measured worst case and below the fp32 reference's.  test_backward_vs_autograd also
+runs the fp32 autograd itself and allows twice its error where that is larger (the c4 plane at K = 50: fp32
+autograd y_bar trimmed 1.8e-3, lambda_bar 1.2e-2, rho_bar 5.5e-2, h_bar 1.8e-2 -- mask flips everywhere)."""
 import numpy as np
 import pytest
 import torch
@@ -25,7 +33,8 @@ CASES = [
     (2, 1, 64, 64, None, 0.05, 0.02, 12, 1e-3),
     (1, 1, 128, 128, ("rand", 10, 10), 0.01, 0.05, 5, 1e-3),
     (1, 1, 16, 32, ("gauss", 3, 0.8), 0.02, 0.1, 1, 1e-3),
-    (2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, 1e-2),   # c2 slices: isolated mask flips
+    (2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, 5e-3),   # c2 slices: isolated mask flips
+    (1, 1, 512, 512, ("gauss", 15, 2.5), 0.0041, 0.021, 50, 1e-3),   # c4 plane at its full K (2-pass adjoint)
 ]
 
 
@@ -38,7 +47,7 @@ def psf(spec, rng):
     return (h / h.sum()).astype(np.float32)
 
 
-def assert_grad(got, ref, what, trim=0.01, tol=1e-4, full_tol=1e-2):
+def assert_grad(got, ref, what, trim=0.01, tol=1e-4, full_tol=5e-3):
     g = np.asarray(got, np.float64).reshape(-1, got.shape[-2] * got.shape[-1])
     r = np.asarray(ref, np.float64).reshape(g.shape)
     assert np.all(np.isfinite(g)), what
@@ -49,6 +58,19 @@ def assert_grad(got, ref, what, trim=0.01, tol=1e-4, full_tol=1e-2):
         full = np.linalg.norm(e) / np.linalg.norm(r[i])
         assert trimmed <= tol, f"{what} plane {i}: trimmed rel-L2 {trimmed:.2e}"
         assert full <= full_tol, f"{what} plane {i}: rel-L2 {full:.2e}"
+
+
+def grad_errs(got, ref, trim=0.01):
+    """(worst trimmed, worst full) per-plane relative L2 of got vs ref."""
+    g = np.asarray(got, np.float64).reshape(-1, got.shape[-2] * got.shape[-1])
+    r = np.asarray(ref, np.float64).reshape(g.shape)
+    tr, fu = 0.0, 0.0
+    for i in range(g.shape[0]):
+        e = g[i] - r[i]
+        keep = np.argsort(np.abs(e))[: int(len(e) * (1 - trim))]
+        tr = max(tr, np.linalg.norm(e[keep]) / np.linalg.norm(r[i][keep]))
+        fu = max(fu, np.linalg.norm(e) / np.linalg.norm(r[i]))
+    return tr, fu
 
 
 def rel(a, b):
@@ -68,13 +90,20 @@ def test_backward_vs_autograd(dev, case):
     torch.cuda.synchronize()
     x0, yb0, hb0, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
                                                         None if h is None else h.astype(np.float64), False, K, xbar)
+    # the same gradients from an fp32 autograd of the oracle: where fp32 rounding flips ST masks (large
+    # planes, many iterations) it differs from fp64 by far more than the case tolerance, and the GPU
+    # (an fp32 implementation too) may then be off by up to twice as much
+    _, yb32, hb32, lb32, rb32 = oracle_torch.tvd_fft_grads(y, np.float32(lam), np.float32(rho), h, False, K, xbar,
+                                                           dtype=torch.float32)
+    t32, f32 = grad_errs(yb32, yb0)
     assert_parity(x.cpu().numpy(), x0, what="x")
-    assert_grad(yb.cpu().numpy(), yb0, "y_bar")
-    assert rel(float(lb), lb0) < stol
-    assert rel(float(rb), rb0) < stol
+    assert_grad(yb.cpu().numpy(), yb0, "y_bar", tol=max(1e-4, 2 * t32), full_tol=max(5e-3, 2 * f32))
+    assert rel(float(lb), lb0) < max(stol, 2 * rel(lb32, lb0))
+    assert rel(float(rb), rb0) < max(stol, 2 * rel(rb32, rb0))
     if h is not None:
         hb = hb.cpu().numpy()
-        assert np.linalg.norm(hb - hb0) / np.linalg.norm(hb0) < stol
+        e32 = np.linalg.norm(hb32 - hb0) / np.linalg.norm(hb0)
+        assert np.linalg.norm(hb - hb0) / np.linalg.norm(hb0) < max(stol, 2 * e32)
 
 
 ISO_CASES = [
@@ -165,8 +194,8 @@ def test_backward_fused_trajectory(dev, with_psf):
     assert_parity(x.cpu().numpy(), x0, what="x")
     assert_grad(yb.cpu().numpy(), yb0, "y_bar")
     assert_grad(yb.cpu().numpy(), yb2.cpu().numpy(), "y_bar fused vs 2-pass trajectory")
-    assert rel(float(lb), lb0) < 1e-2 and rel(float(rb), rb0) < 1e-2
-    assert rel(float(lb), float(lb2)) < 1e-2 and rel(float(rb), float(rb2)) < 1e-2
+    assert rel(float(lb), lb0) < 5e-3 and rel(float(rb), rb0) < 5e-3
+    assert rel(float(lb), float(lb2)) < 5e-3 and rel(float(rb), float(rb2)) < 5e-3
 
 
 @pytest.mark.parametrize("case", [(2, 256, 256, None, False, False), (3, 64, 64, ("gauss", 7, 1.2), False, True),
@@ -230,7 +259,7 @@ def test_backward_fused_adjoint(dev, case):
                                                       None if h is None else h.astype(np.float64), False, K, xbar)
     assert_parity(x.cpu().numpy(), x0, what="x")
     assert_grad(yb_, yb0, "y_bar")
-    assert rel(float(lb), lb0) < 1e-2 and rel(float(rb), rb0) < 1e-2
+    assert rel(float(lb), lb0) < 5e-3 and rel(float(rb), rb0) < 5e-3
 
 
 def test_backward_fused_adjoint_deterministic(dev):

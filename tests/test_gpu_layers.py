@@ -87,3 +87,33 @@ def test_parallel_branches_on_streams_match_serial(dev):
     assert o1.shape == (3, 9, 256, 256)
     assert torch.equal(o1, o2) and torch.equal(g1, g2)
     assert all(torch.equal(a, b) for a, b in zip(l1, l2))
+
+
+def test_c5_denoiser_branch_gradients(dev):
+    """BASELINE c5's caller: the get_denoiser branch of src/nets/net_build.jl:113-128 -- Parallel(chcat) of
+    5 x ADMMDeconvF2((), 50, rho, relu1) -- on a small RGB batch, branches on their own HIP streams.  The
+    gradient of a weighted sum of the output w.r.t. every branch's trainable lambda (deconv_admm.jl:107)
+    against fp64 autograd of the oracle: for branch i, lambda_bar = <xbar_i, d x_i / d lambda> with
+    xbar_i = w_i * relu1'(x_i)."""
+    import oracle_torch
+    rng = np.random.default_rng(12)
+    rhos = (0.002, 0.02, 0.2, 2.0, 4.0)
+    br = [layers.ADMMDeconvF2((), 50, r, layers.relu1, rng=rng, device=dev) for r in rhos]
+    for L in br:
+        L.lam.requires_grad_(True)
+    net = layers.Parallel(layers.chcat, *br)
+    y = synth.make_batch(2, 256, 256, None, P=3, sigma=0.1, g0=9)
+    w = rng.standard_normal((2, 15, 256, 256)).astype(np.float32)
+    out = net(torch.from_numpy(y).to(dev))
+    (out * torch.from_numpy(w).to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    for i, (L, r) in enumerate(zip(br, rhos)):
+        lam = float(L.lam.detach().cpu()[0])
+        x0, _, _, lb0, _ = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(r), None,
+                                                      False, 50, np.zeros(y.shape, np.float32))
+        xbar = w[:, 3 * i:3 * i + 3] * ((x0 > 0) & (x0 < 1))
+        _, _, _, lb0, _ = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(r), None,
+                                                     False, 50, xbar.astype(np.float32))
+        got = float(L.lam.grad.cpu()[0])
+        assert abs(got - lb0) <= 5e-3 * abs(lb0), f"branch {i} (rho {r}): lambda_bar {got} vs {lb0}"
+        np.testing.assert_allclose(out[:, 3 * i:3 * i + 3].detach().cpu().numpy(), np.clip(x0, 0, 1), atol=2e-4)

@@ -154,3 +154,15 @@ def test_iso_couples_batch(dev):
     alone = run_gpu(dev, y[:1], 0.05, 0.05, h, True, 6)
     assert not np.allclose(full[:1], alone, rtol=0, atol=1e-6)
     assert_parity(alone, run_oracle(y[:1], 0.05, 0.05, h, True, 6))
+
+
+def test_c4_full_config_vs_oracle(dev):
+    """BASELINE c4 at its full iteration count: one 512 x 512 RGB image (3 planes), 15 x 15 Gaussian PSF,
+    K = 50, anisotropic (the 2-pass path; the batch's planes are independent, ops.jl:168-173).  The oracle is
+    the spectral form of oracle_np (equal to the literal form to ~1e-14, tests/test_oracle.py)."""
+    h = synth.gaussian_psf(15, 2.5)
+    y = synth.make_batch(1, 512, 512, h, P=3, g0=77)
+    got = run_gpu(dev, y, 0.0041, 0.021, h, False, 50)
+    ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), np.float32(0.0041),
+                                                    np.float32(0.021), oracle_np.psf_from_c(h), False, 50))
+    assert_parity(got, ref, what="c4 512x512x3 K=50")
