@@ -115,8 +115,10 @@ __device__ __forceinline__ void lds_barrier() {
 //   0: clip = min(max(v, -tau), tau); w = |s| > tau ? s - 2 tau sign(s) : -s   (compare + select)
 //   1: clip = med3(v, -tau, tau) (one v_med3_f32); w = s - 2 clip(s) as one FMA (exact: s - 2s = -s,
 //      s - 2 tau sign(s) has one rounding either way)
+// Form 1 is the default since the store-data hazard it exposed is padded at build time (hazard_pad.py;
+// census green, c2 3.34 -> 3.29 ms per solve on one box).
 #ifndef PLANE_PROX
-#define PLANE_PROX 0
+#define PLANE_PROX 1
 #endif
 __device__ __forceinline__ float clip_tau(float v, float tau) {
 #if PLANE_PROX == 1
@@ -283,11 +285,37 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     lds_barrier();
 }
 
+// Line r -/+ 1 of the lane-pair layout is lane t -/+ 2.  PLANE_LANESHIFT 1: two whole-wave DPP shifts
+// (wave_shr:1 / wave_shl:1, VALU) per value; 0: __shfl_up/__shfl_down (a ds_bpermute, i.e. an LDS round
+// trip on the row phase's dependency chain).  Lanes 0,1 (up) / 62,63 (down) receive 0; the callers
+// overwrite them with the boundary lines from LDS.
+#ifndef PLANE_LANESHIFT
+#define PLANE_LANESHIFT 1
+#endif
+__device__ __forceinline__ float lane_up2(float v) {   // lane i <- lane i - 2
+#if PLANE_LANESHIFT
+    __asm__ volatile("" : "+v"(v));
+    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true);
+    return __int_as_float(__builtin_amdgcn_mov_dpp(a, 0x138, 0xF, 0xF, true));
+#else
+    return __shfl_up(v, 2);
+#endif
+}
+__device__ __forceinline__ float lane_down2(float v) {   // lane i <- lane i + 2
+#if PLANE_LANESHIFT
+    __asm__ volatile("" : "+v"(v));
+    const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true);
+    return __int_as_float(__builtin_amdgcn_mov_dpp(a, 0x130, 0xF, 0xF, true));
+#else
+    return __shfl_down(v, 2);
+#endif
+}
+
 // v(register n) = H^T y + rho D^T w, with w of registers n and n+1 (the partner lane's pixel after this
 // lane's last pixel lives one register later on lane A).
 __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, bool hb, bool bot, float rho) {
     const float recv = swapf(hb ? wn.z : wnext.z);     // w2 at the pixel after this lane's 2nd pixel
-    float w1x = __shfl_down(wn.x, 2), w1y = __shfl_down(wn.y, 2);   // w1 of line r+1
+    float w1x = lane_down2(wn.x), w1y = lane_down2(wn.y);   // w1 of line r+1
     if (bot) w1x = w1y = 0.0f;                         // next wave's first line: fixed up after the barrier
     const float q0 = wn.x - w1x + wn.z - wn.w;
     const float q1 = wn.y - w1y + wn.w - recv;
@@ -414,7 +442,7 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
             const float2 x = S[n];
             const float xl = swapf(hb ? (n == 0 ? x63y : S[(n + 63) & 63].y) : x.y);   // pixel before this lane's first
             const float2 xub = xbp[n];
-            float2 xu = make_float2(__shfl_up(x.x, 2), __shfl_up(x.y, 2));   // line r-1
+            float2 xu = make_float2(lane_up2(x.x), lane_up2(x.y));   // line r-1
             xu.x = top ? xub.x : xu.x;
             xu.y = top ? xub.y : xu.y;
             float4 uo = make_float4(clip_tau(so.x, tau), clip_tau(so.y, tau), clip_tau(so.z, tau), clip_tau(so.w, tau));
@@ -482,6 +510,12 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
     }
 }
 
+// timing experiments only (wrong results): skip the column phases (1), the line transforms (2) or the
+// row update (4) of every iteration
+#ifndef PLANE_EXPT_SKIP
+#define PLANE_EXPT_SKIP 0
+#endif
+
 #ifndef PLANE_STAGE_INV
 #define PLANE_STAGE_INV 1
 #endif
@@ -540,9 +574,11 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     line_forward_pair(S, hb);
     dbg_dump<DBG>(dbg, S, 0, t);
     for (int k = 1;; ++k) {
+        if constexpr (!(PLANE_EXPT_SKIP & 1)) {
         column_half<0, 0>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
         if constexpr (DBG == 2) dbg_dump<DBG>(dbg, S, 256 + k, t);
         column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
+        }
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
         // the last iteration keeps x in registers for the output; the others hand x[32..63] to the
         // row phase's LDS staging slots directly (no spill of the line inverse's peak)
@@ -552,7 +588,12 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
             dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
             if (k == K) break;
         } else {
-            line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
+            if constexpr (PLANE_EXPT_SKIP & 2) {
+#pragma unroll
+                for (int m = 0; m < 32; ++m) colbuf[t + m * kPT] = S[32 + m];
+            } else {
+                line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
+            }
             if (k == K) {   // the output needs x[32..63] back (per-thread slots: no barrier)
 #pragma unroll
                 for (int m = 0; m < 16; ++m) S[32 + m] = colbuf[t + m * kPT];
@@ -572,10 +613,15 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
             // ... and s_{K-1} is never read (iteration K stops at x): its stores drop the same way
             const rsrc_t sld = k >= 2 ? sp : make_rsrc(sln, 0);
             const rsrc_t sst = k <= K - 2 ? sp : make_rsrc(sln, 0);
-            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            if constexpr (PLANE_EXPT_SKIP & 4) {
+#pragma unroll
+                for (int m = 0; m < 32; ++m) S[32 + m] = colbuf[t + m * kPT];
+            } else {
+                row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            }
         }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
-        line_forward_pair(S, hb);
+        if constexpr (!(PLANE_EXPT_SKIP & 2)) line_forward_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k, t);
     }
     float2* xrow = reinterpret_cast<float2*>(x_out + plane * 65536 + (size_t)r * 256);
@@ -672,7 +718,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         const float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
         const float2 vub = xbp[n];
-        float2 vu = make_float2(__shfl_up(v.x, 2), __shfl_up(v.y, 2));
+        float2 vu = make_float2(lane_up2(v.x), lane_up2(v.y));
         vu.x = top ? vub.x : vu.x;
         vu.y = top ? vub.y : vu.y;
         const float dv[4] = {v.x - vu.x, v.y - vu.y, v.x - vl, v.y - v.x};

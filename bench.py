@@ -368,7 +368,9 @@ def main():
             "metric": "ADMM deconv images/sec at 256x256 K=25 (% HBM roofline)",
             "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            # c3 fixes the global batch (2048 split over the ranks): strong scaling; c2/c4 fix the per-GPU batch
+            "scaling": "strong" if (config == "c3" and not args.batch) else "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{config}: batch {B}/GPU of {M}x{N}x{P}, {cfg['psf'][0]}x{cfg['psf'][0]} "
                                    f"Gaussian PSF (sigma {cfg['psf'][1]}), K={K}, anisotropic TV, lambda {synth.LAMBDA}, "
                                    f"rho {synth.RHO}", "global_batch": B * world, "image": [M, N, P], "K": K,
