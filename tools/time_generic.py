@@ -18,6 +18,9 @@ for _a in [a for a in sys.argv[1:] if "=" in a]:
     sys.argv.remove(_a)
 
 SHAPES = [(480, 640, 64, 25), (96, 96, 512, 25), (250, 250, 256, 25), (2048, 2048, 8, 25), (256, 256, 512, 25)]
+# positional N,M,B[,K] arguments replace the default shape list (e.g. 250,250,256 for one rocprof run)
+if len(sys.argv) > 1:
+    SHAPES = [tuple(int(v) for v in (a.split(",") + ["25"])[:4]) for a in sys.argv[1:]]
 
 
 def main():
