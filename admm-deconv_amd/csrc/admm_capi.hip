@@ -417,12 +417,15 @@ int gen_opt(int k, int dflt) {
     return v >= 256 && v <= 8192 ? v : dflt;
 }
 int gen_T(int M, int N) {
-    // 2048: smaller blocks, more of them resident per CU (480x640: 1.3x over 4096, tools/gen_knobs.sh)
+    // 2048: smaller blocks, more of them resident per CU (480x640: 1.3x over 4096, tools/gen_knobs.sh).
+    // T need not divide N (ragged last block): 250 x 250 ran 2-line blocks when it had to.
     const int tm = gen_opt(ADMM_OPT_GEN_TM, 2048);
     for (int t = 8; t > 1; t >>= 1)
-        if (N % t == 0 && t * M <= tm) return t;
+        if (t * M <= tm && t <= N) return t;
     return 1;
 }
+// line blocks per plane: the last block of a plane may hold fewer than T lines (N need not divide by T)
+int gen_nb(int N, int T) { return (N + T - 1) / T; }
 int gen_KB(int M, int N) {
     // 1024 points per column block: with the XCD-aware block order, smaller blocks won at every size
     // measured (480x640 column pass 3.29 -> 2.92 ms; 256 / 512 / 2048+ slower, tools/time_generic.py)
@@ -612,7 +615,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     const float* prm = reinterpret_cast<const float*>(ws + lay.prm);
     const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
     const int T = gen_T(M, N), KB = gen_KB(M, N);
-    const dim3 gl(N / T, (unsigned)planes), gc((H + KB - 1) / KB, (unsigned)planes);
+    const dim3 gl(gen_nb(N, T), (unsigned)planes), gc((H + KB - 1) / KB, (unsigned)planes);
     const size_t lfw = gen_lds_line(M, T, false);                    // line_fwd / line_inv
     const size_t lup = gen_lds_line(M, T, true);                     // line_upd / iso_b
     const size_t lcol = gen_lds_col(N, KB);
@@ -674,7 +677,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         }
         float* nrm_out = tr.nrm ? tr.nrm + (size_t)(it - 1) * MN : nullptr;
         rc = ln.run(ADMM_K_LINE, [&] {
-            hipLaunchKernelGGL(g::iso_a_kernel, dim3(N / T, ng), dim3(256), (size_t)T * M * 4, s, xg, s_in, sa, fmap,
+            hipLaunchKernelGGL(g::iso_a_kernel, dim3(gen_nb(N, T), ng), dim3(256), (size_t)T * M * 4, s, xg, s_in, sa, fmap,
                                part, M, N, (int)planes, iso_group(planes), T, it == 1 ? 1 : 0);
         });
         if (rc) return rc;
@@ -758,11 +761,11 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
         b.wbar = take(planes * MN * 4);   // vbar_k handed from ISO_ADJ_A to ISO_ADJ_B
         b.Rmap = take(MN * 4);
         b.Rpart = take(ng * MN * 4);
-        b.nblk_isoA = (int)(ng * (N / T));
+        b.nblk_isoA = (int)(ng * gen_nb(N, T));
         b.nblk_isoR = kIsoAdjRBlocks;
         b.nblk_line = b.nblk_isoA + b.nblk_isoR;
     } else {
-        b.nblk_line = (int)(planes * (N / T));
+        b.nblk_line = (int)(planes * gen_nb(N, T));
     }
     b.rpart = take((size_t)K * b.nblk_line * 2 * 8);
     b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 4) : 0;
@@ -1040,7 +1043,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         namespace g = admm::gen;
         const int H = M / 2 + 1;
         const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
-        const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
+        const dim3 ggl(gen_nb(N, T), (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
         const size_t lfw = gen_lds_line(M, T, false), lup = gen_lds_line(M, T, true);
         const size_t lcol = gen_lds_col(N, KB);
         set_lds(g::line_fwd_kernel, lfw);
@@ -1075,7 +1078,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             }
             const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
             rc = ln.run(ADMM_K_ADJ, [&] {
-                hipLaunchKernelGGL(g::iso_adj_a_kernel, dim3(N / T, (unsigned)ngi), dim3(256), (size_t)T * M * 4, s, vb,
+                hipLaunchKernelGGL(g::iso_adj_a_kernel, dim3(gen_nb(N, T), (unsigned)ngi), dim3(256), (size_t)T * M * 4, s, vb,
                                    sk1, skk, xK, nrm1, sbi, wbar, vsum, Rpart, rp, M, N, (int)planes, iso_group(planes),
                                    T, prm);
             });
@@ -1158,7 +1161,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             namespace g = admm::gen;
             const int H = M / 2 + 1;
             const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
-            const dim3 ggl(N / T, (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
+            const dim3 ggl(gen_nb(N, T), (unsigned)planes), ggc((H + KB - 1) / KB, (unsigned)planes);
             const size_t lfw = gen_lds_line(M, T, false), lcol = gen_lds_col(N, KB);
             rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, ggl, dim3(256), lfw, s, vsum, specA, twM, pM, N, T); });
             if (rc) return rc;

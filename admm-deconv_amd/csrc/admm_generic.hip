@@ -114,12 +114,39 @@ __device__ __forceinline__ void bfly_any(const float2* __restrict__ src, float2*
     }
 }
 
+// LDS hand-off between the lanes of one wave: a wave's LDS instructions execute in order; the fences keep
+// the compiler from moving this pass's loads above the previous pass's stores.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void wave_pass(const float2* __restrict__ src, float2* __restrict__ dst, int lane, int q,
+                                          int Ns, int tstep, const float2* __restrict__ tw) {
+    for (int j = lane; j < q; j += 64) bfly<R, INV>(src, dst, j, q, Ns, tstep, tw);
+}
+
 // cnt transforms of length pl.n at a[t * stride ...]; ping-pong with b; returns the buffer holding the
-// result.  The caller synchronises before (input ready) -- every pass ends with a block barrier.
+// result.  One WAVE per transform (transform t on wave t mod nwaves): the passes of a transform hand off
+// through LDS with wave-level ordering only, so the block's waves run their transforms without block
+// barriers between passes (a 250-point line is 4 passes of 50..125 butterflies: per-pass block barriers
+// were most of its time).  The caller synchronises before (input ready); this ends with a block barrier.
+// GEN_WAVE_FFT 1 (default): per-wave passes when every wave has a transform and transforms are long
+// enough to fill a wave's lanes (n >= 128), else block-wide passes; 0: always block-wide; 2: always per-wave.
+// Measured (1x MI355X, K=25, tools/gen_variants.sh): per-wave 250^2 40.3k img/s vs block-wide 36.8k; 96^2
+// 182k vs 225k (12..48-butterfly passes), 2048^2 206 vs 292 (one transform per column block).
+#ifndef GEN_WAVE_FFT
+#define GEN_WAVE_FFT 1
+#endif
 template <bool INV>
 __device__ float2* fft(float2* a, float2* b, int cnt, int stride, const FPlan& pl, const float2* __restrict__ tw) {
-    int Ns = 1;
     const int n = pl.n;
+    const bool wave_mode = GEN_WAVE_FFT == 2 || (GEN_WAVE_FFT == 1 && cnt >= (int)(blockDim.x >> 6) && n >= 128);
+    if (!wave_mode) {
+    // block-wide passes (one block barrier per pass): every thread takes butterflies of every transform
+    int Ns = 1;
     for (int p = 0; p < pl.nf; ++p) {
         const int R = pl.r[p];
         const int q = n / R;
@@ -144,7 +171,59 @@ __device__ float2* fft(float2* a, float2* b, int cnt, int stride, const FPlan& p
         b = t;
     }
     return a;
+    }
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int f = threadIdx.x >> 6; f < cnt; f += nw) {
+        const float2* src = a + (size_t)f * stride;
+        float2* dst = b + (size_t)f * stride;
+        int Ns = 1;
+        for (int p = 0; p < pl.nf; ++p) {
+            const int R = pl.r[p];
+            const int q = n / R;
+            const int tstep = n / (Ns * R);
+            switch (R) {
+                case 2: wave_pass<2, INV>(src, dst, lane, q, Ns, tstep, tw); break;
+                case 3: wave_pass<3, INV>(src, dst, lane, q, Ns, tstep, tw); break;
+                case 4: wave_pass<4, INV>(src, dst, lane, q, Ns, tstep, tw); break;
+                case 5: wave_pass<5, INV>(src, dst, lane, q, Ns, tstep, tw); break;
+                case 8: wave_pass<8, INV>(src, dst, lane, q, Ns, tstep, tw); break;
+                default:
+                    for (int j = lane; j < q; j += 64) bfly_any<INV>(src, dst, j, q, Ns, R, n, tstep, tw);
+                    break;
+            }
+            wave_sync();
+            Ns *= R;
+            const float2* t = dst;
+            dst = const_cast<float2*>(src);
+            src = t;
+        }
+    }
+    __syncthreads();
+    return (pl.nf & 1) ? b : a;
 }
+
+// Block-stride loop over [0, total) that issues the global loads of U consecutive strides before any of
+// their uses.  A plain loop whose body loads global memory and stores LDS runs one load latency per
+// stride (the compiler does not pipeline across the LDS stores); SQ counters of the 250 x 250 line
+// kernels showed their waves waiting most of their lifetime.
+template <int U, class Load, class Use>
+__device__ __forceinline__ void batched(int total, Load&& load, Use&& use) {
+    using V = decltype(load(0));
+    for (int b = threadIdx.x; b < total; b += U * (int)blockDim.x) {
+        V v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x;
+            if (i < total) v[u] = load(i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = b + u * (int)blockDim.x;
+            if (i < total) use(i, v[u]);
+        }
+    }
+}
+constexpr int kU = 4;
 
 __device__ __forceinline__ int wrap(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
@@ -184,19 +263,20 @@ __device__ __forceinline__ float phi(float s, float tau) { return fabsf(s) > tau
 
 // real lines -> half spectra (T lines per block, grid (N / T, planes))
 __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__ src, float2* __restrict__ spec,
-                                                       const float2* __restrict__ twM, FPlan pM, int N, int T) {
+                                                       const float2* __restrict__ twM, FPlan pM, int N, int Tg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float2* B = A + (size_t)((Tg + 1) / 2) * M;   // P = ceil(Tg / 2) paired transforms
     const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
-    const int plane = xb.y, j0 = xb.x * T;
+    const int plane = xb.y, j0 = xb.x * Tg;
+    const int T = min(Tg, N - j0);   // the last block of a plane may be ragged (gen_nb)
     const float* sp = src + ((size_t)plane * N + j0) * M;
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((Tg + 1) / 2) * M, twM, M);
+    batched<kU>(T * M, [&](int idx) { return sp[idx]; }, [&](int idx, float v) {
         const int t = fdiv(idx, M);
-        pack_real(A, t, idx - t * M, M, sp[idx]);
-    }
+        pack_real(A, t, idx - t * M, M, v);
+    });
     pad_odd(A, T, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
@@ -205,27 +285,28 @@ __global__ __launch_bounds__(256) void line_fwd_kernel(const float* __restrict__
 
 // half spectra -> real lines (Hermitian extension, complex inverse, real part; unnormalised)
 __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict__ spec, float* __restrict__ dst,
-                                                       const float2* __restrict__ twM, FPlan pM, int N, int T) {
+                                                       const float2* __restrict__ twM, FPlan pM, int N, int Tg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
+    float2* B = A + (size_t)((Tg + 1) / 2) * M;   // P = ceil(Tg / 2) paired transforms
     const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
-    const int plane = xb.y, j0 = xb.x * T;
+    const int plane = xb.y, j0 = xb.x * Tg;
+    const int T = min(Tg, N - j0);   // the last block of a plane may be ragged (gen_nb)
     const float2* sp = spec + ((size_t)plane * N + j0) * H;
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((Tg + 1) / 2) * M, twM, M);
     // two lines per transform: Z = X_2p + i X_2p+1 (Hermitian extensions, DC / Nyquist bins taken real,
     // which is what the real part of one line's inverse keeps) -> z = x_2p + i x_2p+1
     const int P = (T + 1) / 2;
-    for (int idx = threadIdx.x; idx < P * M; idx += blockDim.x) {
+    batched<kU>(P * M, [&](int idx) {
         const int p = fdiv(idx, M), k = idx - p * M;
         const float2* sa = sp + (size_t)(2 * p) * H;
         float2 ev = k < H ? sa[k] : cconj(sa[M - k]);   // line 2p
         float2 od = make_float2(0.0f, 0.0f);             // line 2p + 1
         if (2 * p + 1 < T) od = k < H ? sa[H + k] : cconj(sa[H + M - k]);
         if (k == 0 || 2 * k == M) ev.y = od.y = 0.0f;
-        A[idx] = make_float2(ev.x - od.y, ev.y + od.x);
-    }
+        return make_float2(ev.x - od.y, ev.y + od.x);
+    }, [&](int idx, float2 v) { A[idx] = v; });
     __syncthreads();
     const float2* R = fft<true>(A, B, P, M, pM, tw);
     float* dp = dst + ((size_t)plane * N + j0) * M;
@@ -256,10 +337,13 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
     const float2* sp = src + (size_t)plane * N * H + k0;
     float2* dp = dst + (size_t)plane * N * H + k0;
     const float2* tw = stage_tw(smem_raw, (size_t)16 * KB * N, twN, N);
-    for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
+    batched<kU>(N * KB, [&](int idx) {
         const int j = fdiv(idx, KB), c = idx - j * KB;
-        A[c * N + j] = c < kc ? sp[(size_t)j * H + c] : make_float2(0.f, 0.f);
-    }
+        return c < kc ? sp[(size_t)j * H + c] : make_float2(0.f, 0.f);
+    }, [&](int idx, float2 v) {
+        const int j = fdiv(idx, KB), c = idx - j * KB;
+        A[c * N + j] = v;
+    });
     __syncthreads();
     float2* R = fft<false>(A, B, KB, N, pN, tw);
     float2* O = R == A ? B : A;
@@ -290,43 +374,56 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
 __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__ x, const float* __restrict__ s_old,
                                                        float* __restrict__ s_new, const float* __restrict__ hty,
                                                        float2* __restrict__ spec, const float2* __restrict__ twM,
-                                                       FPlan pM, int N, int T, const float* __restrict__ prm, int first) {
+                                                       FPlan pM, int N, int Tg, const float* __restrict__ prm, int first) {
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
-    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);   // T+1 lines
-    float* W1 = W0 + (size_t)(T + 1) * M;                       // T lines
+    float2* B = A + (size_t)((Tg + 1) / 2) * M;   // P = ceil(Tg / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((Tg + 1) / 2) * M);   // Tg+1 lines
+    float* W1 = W0 + (size_t)(Tg + 1) * M;                       // Tg lines
     const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
-    const int plane = xb.y, j0 = xb.x * T;
+    const int plane = xb.y, j0 = xb.x * Tg;
+    const int T = min(Tg, N - j0);   // the last block of a plane may be ragged (gen_nb)
     const float* xp = x + (size_t)plane * MN;
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
-    for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
+    struct UpdIn {
+        float xc, xu, xl, a0, a1;
+    };
+    batched<kU>((T + 1) * M, [&](int idx) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const int jj = wrap(j0 + t, N), jp = wrap(jj - 1, N);
         const size_t o = (size_t)jj * M + i;
-        const float xc = xp[o];
-        const float s0 = xc - xp[(size_t)jp * M + i] + (first ? 0.0f : clip(so[o], tau));
+        UpdIn r;
+        r.xc = xp[o];
+        r.xu = xp[(size_t)jp * M + i];
+        r.xl = t < T ? xp[(size_t)jj * M + wrap(i - 1, M)] : 0.0f;
+        r.a0 = first ? 0.0f : so[o];
+        r.a1 = (first || t >= T) ? 0.0f : so[MN + o];
+        return r;
+    }, [&](int idx, const UpdIn& r) {
+        const int t = fdiv(idx, M), i = idx - t * M;
+        const size_t o = (size_t)wrap(j0 + t, N) * M + i;
+        const float s0 = r.xc - r.xu + (first ? 0.0f : clip(r.a0, tau));
         W0[idx] = phi(s0, tau);
         if (t < T) {
-            const float s1 = xc - xp[(size_t)jj * M + wrap(i - 1, M)] + (first ? 0.0f : clip(so[MN + o], tau));
+            const float s1 = r.xc - r.xl + (first ? 0.0f : clip(r.a1, tau));
             W1[idx] = phi(s1, tau);
             sn[o] = s0;
             sn[MN + o] = s1;
         }
-    }
+    });
     __syncthreads();
     const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+    batched<kU>(T * M, [&](int idx) { return hp[idx]; }, [&](int idx, float hv) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
-    }
+        pack_real(A, t, i, M, fmaf(rho, dtw, hv));
+    });
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((Tg + 1) / 2) * M + (size_t)4 * (2 * Tg + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
@@ -337,30 +434,42 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
 // group's partial sum of s^2 over planes and both channels per pixel (ops.jl:6)
 __global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x, const float* s_in, float* s,
                                                     const float* __restrict__ fmap, float* __restrict__ part, int M,
-                                                    int N, int planes, int G, int T, int first) {
+                                                    int N, int planes, int G, int Tg, int first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float* acc = reinterpret_cast<float*>(smem_raw);
     const size_t MN = (size_t)M * N;
-    const int j0 = blockIdx.x * T, grp = blockIdx.y;
+    const int j0 = blockIdx.x * Tg, grp = blockIdx.y;
+    const int T = min(Tg, N - j0);   // the last block may be ragged (gen_nb)
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) acc[idx] = 0.0f;
     const int p_end = min(planes, (grp + 1) * G);
     for (int plane = grp * G; plane < p_end; ++plane) {
         const float* xp = x + (size_t)plane * MN;
         float* sp = s + (size_t)plane * 2 * MN;
         const float* si = s_in + (size_t)plane * 2 * MN;   // s_in may alias s (same element read first)
-        for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+        struct IsoIn {
+            float f, xc, xu, xl, a0, a1;
+        };
+        batched<kU>(T * M, [&](int idx) {
             const int t = fdiv(idx, M), i = idx - t * M;
             const int jj = j0 + t, jp = wrap(jj - 1, N);
             const size_t o = (size_t)jj * M + i;
-            const float f = first ? 0.0f : fmap[o];
-            const float xc = xp[o];
-            const float a0 = first ? 0.0f : si[o], a1 = first ? 0.0f : si[MN + o];
-            const float s0 = (xc - xp[(size_t)jp * M + i]) + (a0 - f * a0);
-            const float s1 = (xc - xp[(size_t)jj * M + wrap(i - 1, M)]) + (a1 - f * a1);
+            IsoIn r;
+            r.f = first ? 0.0f : fmap[o];
+            r.xc = xp[o];
+            r.xu = xp[(size_t)jp * M + i];
+            r.xl = xp[(size_t)jj * M + wrap(i - 1, M)];
+            r.a0 = first ? 0.0f : si[o];
+            r.a1 = first ? 0.0f : si[MN + o];
+            return r;
+        }, [&](int idx, const IsoIn& r) {
+            const int t = fdiv(idx, M), i = idx - t * M;
+            const size_t o = (size_t)(j0 + t) * M + i;
+            const float s0 = (r.xc - r.xu) + (r.a0 - r.f * r.a0);
+            const float s1 = (r.xc - r.xl) + (r.a1 - r.f * r.a1);
             sp[o] = s0;
             sp[MN + o] = s1;
             acc[idx] += s0 * s0 + s1 * s1;   // each idx is owned by one thread
-        }
+        });
     }
     float* pp = part + (size_t)grp * MN + (size_t)j0 * M;
     for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) pp[idx] = acc[idx];
@@ -369,35 +478,38 @@ __global__ __launch_bounds__(256) void iso_a_kernel(const float* __restrict__ x,
 // isotropic step B: w = (2f - 1) s, v = H^T y + rho D^T w -> half spectrum
 __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s, const float* __restrict__ fmap,
                                                     const float* __restrict__ hty, float2* __restrict__ spec,
-                                                    const float2* __restrict__ twM, FPlan pM, int N, int T,
+                                                    const float2* __restrict__ twM, FPlan pM, int N, int Tg,
                                                     const float* __restrict__ prm) {
     const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
     float2* A = reinterpret_cast<float2*>(smem_raw);
-    float2* B = A + (size_t)((T + 1) / 2) * M;   // P = ceil(T / 2) paired transforms
-    float* W0 = reinterpret_cast<float*>(B + (size_t)((T + 1) / 2) * M);
-    float* W1 = W0 + (size_t)(T + 1) * M;
+    float2* B = A + (size_t)((Tg + 1) / 2) * M;   // P = ceil(Tg / 2) paired transforms
+    float* W0 = reinterpret_cast<float*>(B + (size_t)((Tg + 1) / 2) * M);
+    float* W1 = W0 + (size_t)(Tg + 1) * M;
     const XBlk xb = xcd_block();   // XCD-aware block order (admm_kernels.hip): neighbours share L2 lines
-    const int plane = xb.y, j0 = xb.x * T;
+    const int plane = xb.y, j0 = xb.x * Tg;
+    const int T = min(Tg, N - j0);   // the last block of a plane may be ragged (gen_nb)
     const float* sp = s + (size_t)plane * 2 * MN;
-    for (int idx = threadIdx.x; idx < (T + 1) * M; idx += blockDim.x) {
+    batched<kU>((T + 1) * M, [&](int idx) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const size_t o = (size_t)wrap(j0 + t, N) * M + i;
-        const float f = fmap[o];
-        W0[idx] = f * sp[o] - (sp[o] - f * sp[o]);
-        if (t < T) W1[idx] = f * sp[MN + o] - (sp[MN + o] - f * sp[MN + o]);
-    }
+        return make_float3(fmap[o], sp[o], t < T ? sp[MN + o] : 0.0f);
+    }, [&](int idx, float3 r) {
+        const int t = fdiv(idx, M);
+        W0[idx] = r.x * r.y - (r.y - r.x * r.y);
+        if (t < T) W1[idx] = r.x * r.z - (r.z - r.x * r.z);
+    });
     __syncthreads();
     const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
-    for (int idx = threadIdx.x; idx < T * M; idx += blockDim.x) {
+    batched<kU>(T * M, [&](int idx) { return hp[idx]; }, [&](int idx, float hv) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
-        pack_real(A, t, i, M, fmaf(rho, dtw, hp[idx]));
-    }
+        pack_real(A, t, i, M, fmaf(rho, dtw, hv));
+    });
     pad_odd(A, T, M);
-    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((T + 1) / 2) * M + (size_t)4 * (2 * T + 1) * M, twM, M);
+    const float2* tw = stage_tw(smem_raw, (size_t)16 * ((Tg + 1) / 2) * M + (size_t)4 * (2 * Tg + 1) * M, twM, M);
     __syncthreads();
     const float2* R = fft<false>(A, B, (T + 1) / 2, M, pM, tw);
     store_real_spectra(R, spec + ((size_t)plane * N + j0) * H, T, M);
