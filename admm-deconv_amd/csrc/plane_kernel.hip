@@ -198,10 +198,17 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     // multipliers for this thread's 32 bins (coalesced, L2-resident), issued once v is dead so they do
     // not add to the register peak of the FFT
     sched_fence();
+    // MODE 1 (H^T y, once per solve) loads its complex multipliers in two halves of 16 (PLANE_GF_SPLIT):
+    // all 32 at once (64 VGPRs) set the PSF kernel's register peak and its allocation spilled inside the
+    // iteration loop as well
+#ifndef PLANE_GF_SPLIT
+#define PLANE_GF_SPLIT 1
+#endif
+    constexpr int NGF = (MODE == 1 && PLANE_GF_SPLIT) ? 16 : 32;
     float cf[MODE == 0 ? 32 : 1];
     float2 gf[MODE == 1 ? 32 : 1];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < NGF; ++j) {
 #ifdef PLANE_EXPT_NOCF
         // timing experiment only (wrong results): no multiplier loads in the x-update column phase
         if constexpr (MODE == 0) { cf[j] = 1.0f / 65536.0f; continue; }
@@ -238,12 +245,20 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
         *m256 = u[0][0];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (MODE == 1 && NGF == 16) {
+            if (i == 2) {   // second half of the complex multipliers, into the slots of the first
+                sched_fence();
+#pragma unroll
+                for (int j = 0; j < 16; ++j) gf[j] = bld2(Gf, t * 8, (HALF * 32 + 16 + j) * kPT * 8);
+            }
+        }
 #pragma unroll
         for (int q2 = 0; q2 < 8; ++q2) {
             if constexpr (MODE == 0) u[i][q2] = cscale(u[i][q2], cf[i * 8 + q2]);
-            else u[i][q2] = cmul(u[i][q2], gf[i * 8 + q2]);
+            else u[i][q2] = cmul(u[i][q2], gf[(i * 8 + q2) % NGF]);
         }
+    }
     if (wave0) {
         wave_lds_sync();
         const float2* mr = mir + (8 - q);
@@ -567,7 +582,11 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     if constexpr (PSF) {
         line_forward_pair(S, hb);
         column_phase<1>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
-        line_inverse_pair(S, hb);   // = H^T y (the 1/(MN) is in Gf)
+        // = H^T y (the 1/(MN) is in Gf).  Staged as in the iterations (x[32..63] through per-thread LDS
+        // slots, no barrier): the unstaged inverse's peak exceeds 256 VGPRs and spilled.
+        line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
+#pragma unroll
+        for (int m = 0; m < 32; ++m) S[32 + m] = colbuf[t + m * kPT];
     }
 #pragma unroll
     for (int n = 0; n < 64; ++n) bst2(hp, t * 8, n * kPT * 8, S[n]);
