@@ -358,10 +358,11 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
 #endif
     constexpr int CH = PLANE_CH;     // registers per chunk
 #ifndef PLANE_PD
-#define PLANE_PD 1
+#define PLANE_PD 2
 #endif
-    // Prefetch distance (chunks in flight).  PD > 1 measured no faster and, with the PSF variant's
-    // register allocation, reproduced the VMEM-overwrites-DPP-source corruption.
+    // Prefetch distance (chunks in flight).  Round 1's PD > 1 builds hit the store-data hazard that
+    // hazard_pad.py now pads; padded, PD = 2 passes the census and is the fastest
+    // (c2 3.31 -> 3.20 ms; PD = 3 3.22, CH = 4 3.21).
     constexpr int PD = PLANE_PD;
     constexpr int NCH = 64 / CH;
     const int lane = t & 63, w = t >> 6;

@@ -214,16 +214,34 @@ def cpu_baseline(cfg, psf, base, target_s):
     }
 
 
-def load_traffic(cfg_name, kernel):
+def load_traffic(cfg_name, kernel, key="hbm_bytes_per_launch"):
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         e = d.get(cfg_name, {}).get(kernel)
-        return None if e is None else e.get("hbm_bytes_per_launch")
+        return None if e is None else e.get(key)
     except Exception:
         return None
+
+
+# VALU issue peak: 4 SIMDs per CU, each issuing a wave64 fp32 VALU instruction every 2 cycles
+# (MI355X_MICROARCH.md, per-instruction constants), 256 CUs, 2.4 GHz
+VALU_ISSUE_PEAK = 256 * 2 * 2.4e9   # wave-instructions per second
+
+
+def compute_side(cfg_name, kernel, avg_ms):
+    """Compute-side figure of the dominant kernel: SQ_INSTS_VALU per launch (PMC, profiles/pmc_traffic.json)
+    over the chip's VALU issue peak for the measured launch time."""
+    valu = load_traffic(cfg_name, kernel, "valu_insts_per_launch")
+    if not valu:
+        return None
+    rate = valu / (avg_ms * 1e-3)
+    return {"valu_insts_per_launch": valu, "valu_issue_rate": rate, "valu_issue_peak": VALU_ISSUE_PEAK,
+            "valu_issue_frac": round(rate / VALU_ISSUE_PEAK, 4),
+            "lds_insts_per_launch": load_traffic(cfg_name, kernel, "lds_insts_per_launch"),
+            "wait_any_frac": load_traffic(cfg_name, kernel, "wait_any_frac")}
 
 
 def spawn_ranks(n):
@@ -348,6 +366,7 @@ def main():
         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
         "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
         "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
+        "compute": compute_side(config, dom, kernels[dom]["avg_ms"]),
         "whole_solve": {
             # the bytes of the path that ran (fused: plane_bytes_per_px; 2-pass: SURVEY s8d canonical)
             "algorithmic_bytes": alg_bytes,

@@ -1,6 +1,6 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes per kernel class.
 
-usage: python tools/make_traffic.py CONFIG OUT.json gpurun_out/prof_TAG/pmc_fetch gpurun_out/prof_TAG/pmc_write
+usage: python tools/make_traffic.py CONFIG OUT.json gpurun_out/prof_TAG/pmc_fetch gpurun_out/prof_TAG/pmc_write [pmc_sq]
 
 hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (FETCH_SIZE reads half the bytes of
 a wide coalesced stream on gfx950 -- MI355X_MICROARCH.md, HBM section; WRITE_SIZE is exact for 16-B
@@ -32,6 +32,7 @@ def klass(name):
 
 def main():
     cfg, out, fdir, wdir = sys.argv[1:5]
+    sq = load([sys.argv[5]]) if len(sys.argv) > 5 else {}
     f = load([fdir])
     w = load([wdir])
     res = json.load(open(out)) if os.path.exists(out) else {}
@@ -45,7 +46,15 @@ def main():
         ent[c] = {"kernel": name, "fetch_size_kib": fs, "write_size_kib": ws,
                   "hbm_bytes_per_launch": int(2 * fs * 1024 + ws * 1024),
                   "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 correction); includes Infinity-Cache hits"}
-        print(cfg, c, ent[c]["hbm_bytes_per_launch"])
+        if name in sq and "SQ_INSTS_VALU" in sq[name]:
+            avg = lambda k: sum(sq[name][k]) / len(sq[name][k])
+            # wave-level instruction counts per launch (SQ counters sum over the whole chip)
+            ent[c]["valu_insts_per_launch"] = avg("SQ_INSTS_VALU")
+            ent[c]["lds_insts_per_launch"] = avg("SQ_INSTS_LDS")
+            ent[c]["salu_insts_per_launch"] = avg("SQ_INSTS_SALU")
+            ent[c]["waves_per_launch"] = avg("SQ_WAVES")
+            ent[c]["wait_any_frac"] = avg("SQ_WAIT_ANY") / max(avg("SQ_WAVE_CYCLES"), 1.0)
+        print(cfg, c, ent[c]["hbm_bytes_per_launch"], ent[c].get("valu_insts_per_launch"))
     json.dump(res, open(out, "w"), indent=1)
 
 
