@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "line_pair.hpp"
+#include "line_quad.hpp"
 #include "plane_kernel.hip"
 
 namespace {
@@ -32,6 +33,69 @@ __global__ __launch_bounds__(512) void pair_inv_kernel(const float2* __restrict_
     float2* row = reinterpret_cast<float2*>(x + (size_t)r * 256) + (hb ? 1 : 0);
 #pragma unroll
     for (int n = 0; n < 64; ++n) row[2 * n] = S[n];
+}
+
+// lane-quad layout: one block = 1024 threads = 256 lines
+__global__ __launch_bounds__(1024) void quad_fwd_kernel(const float* __restrict__ x, float2* __restrict__ spec) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 2);
+    const admm::quad::Lane L = admm::quad::lane_of(threadIdx.x);
+    const float2* row = reinterpret_cast<const float2*>(x + (size_t)r * 256) + L.q;
+    float2 S[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) S[m] = row[4 * m];
+    admm::quad::line_forward(S, L);
+    float2* out = spec + (size_t)r * 128 + 32 * L.p;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) out[k] = S[k];
+}
+
+__global__ __launch_bounds__(1024) void quad_inv_kernel(const float2* __restrict__ spec, float* __restrict__ x) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 2);
+    const admm::quad::Lane L = admm::quad::lane_of(threadIdx.x);
+    const float2* in = spec + (size_t)r * 128 + 32 * L.p;
+    float2 S[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) S[k] = in[k];
+    admm::quad::line_inverse(S, L);
+    float2* row = reinterpret_cast<float2*>(x + (size_t)r * 256) + L.q;
+#pragma unroll
+    for (int m = 0; m < 32; ++m) row[4 * m] = S[m];
+}
+
+// timing: `reps` inverse + forward round trips of every line in registers (scaled by 1/256 each time)
+__global__ __launch_bounds__(1024) void quad_bench_kernel(const float* __restrict__ x, float* __restrict__ y, int reps) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 2);
+    const admm::quad::Lane L = admm::quad::lane_of(threadIdx.x);
+    const float2* row = reinterpret_cast<const float2*>(x + (size_t)r * 256) + L.q;
+    float2 S[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) S[m] = row[4 * m];
+    for (int i = 0; i < reps; ++i) {
+        admm::quad::line_forward(S, L);
+        admm::quad::line_inverse(S, L);
+#pragma unroll
+        for (int m = 0; m < 32; ++m) S[m] = admm::cscale(S[m], 1.0f / 256.0f);
+    }
+    float2* o = reinterpret_cast<float2*>(y + (size_t)r * 256) + L.q;
+#pragma unroll
+    for (int m = 0; m < 32; ++m) o[4 * m] = S[m];
+}
+__global__ __launch_bounds__(512) void pair_bench_kernel(const float* __restrict__ x, float* __restrict__ y, int reps) {
+    const int r = blockIdx.x * 256 + (threadIdx.x >> 1);
+    const bool hb = threadIdx.x & 1;
+    const float2* row = reinterpret_cast<const float2*>(x + (size_t)r * 256) + (hb ? 1 : 0);
+    float2 S[64];
+#pragma unroll
+    for (int n = 0; n < 64; ++n) S[n] = row[2 * n];
+    for (int i = 0; i < reps; ++i) {
+        admm::line_forward_pair(S, hb);
+        admm::line_inverse_pair(S, hb);
+#pragma unroll
+        for (int n = 0; n < 64; ++n) S[n] = admm::cscale(S[n], 1.0f / 256.0f);
+    }
+    float2* o = reinterpret_cast<float2*>(y + (size_t)r * 256) + (hb ? 1 : 0);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) o[2 * n] = S[n];
 }
 
 }  // namespace
@@ -91,6 +155,29 @@ int devtest_plane_debug_psf(const float* y, float* x, const float* Cf, const flo
 int devtest_pair_forward(const float* x, float* spec, int rows) {
     pair_fwd_kernel<<<rows / 256, 512>>>(x, reinterpret_cast<float2*>(spec));
     return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+int devtest_quad_forward(const float* x, float* spec, int rows) {
+    quad_fwd_kernel<<<rows / 256, 1024>>>(x, reinterpret_cast<float2*>(spec));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+int devtest_quad_inverse(const float* spec, float* x, int rows) {
+    quad_inv_kernel<<<rows / 256, 1024>>>(reinterpret_cast<const float2*>(spec), x);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -4;
+}
+// line-transform round trips, lane-quad (quad = 1) or lane-pair layout; returns kernel ms through *ms
+int devtest_line_bench(const float* x, float* y, int rows, int reps, int quad, float* ms) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a);
+    if (quad) quad_bench_kernel<<<rows / 256, 1024>>>(x, y, reps);
+    else pair_bench_kernel<<<rows / 256, 512>>>(x, y, reps);
+    hipEventRecord(b);
+    const bool ok = hipEventSynchronize(b) == hipSuccess;
+    hipEventElapsedTime(ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return ok ? 0 : -4;
 }
 int devtest_pair_inverse(const float* spec, float* x, int rows) {
     pair_inv_kernel<<<rows / 256, 512>>>(reinterpret_cast<const float2*>(spec), x);
