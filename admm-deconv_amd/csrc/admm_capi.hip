@@ -26,6 +26,7 @@
 #include "admm_backward.hip"
 #include "admm_generic_bwd.hip"
 #include "plane_api.hpp"
+#include "smooth_api.hpp"
 
 namespace {
 
@@ -68,7 +69,7 @@ constexpr int kGenMax = 4096;
 // Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
 // choices; the others exist for tests (fused vs 2-pass) and tuning experiments.  A recording stores
 // the option values it was made with, and its replay rejects a change (RecTag below).
-std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}};
+std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
 int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 
 // The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox;
@@ -641,17 +642,25 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     }
     const int ng = iso_ngroups(planes);
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
+    // per-iteration kernels with compile-time plans where this build has the length (admm_smooth.hip):
+    // the column pass needs N, the line passes M
+    const bool smc = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(N);
+    const bool sml = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(M);
     for (int it = 1; it <= maxit; ++it) {
         // trajectory for h_bar: the dim-2 spectrum of iteration it before the multiply
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * planes * N * H : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
+            if (smc && !vsave) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, twN, 1.0f, opt(ADMM_OPT_SMOOTH));
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB,
                                vsave ? 4 : 0, 1.0f, vsave, (float*)nullptr);
+            return 0;
         });
         if (rc) return rc;
         const bool last = it == maxit;
         rc = ln.run(last ? ADMM_K_FINAL : ADMM_K_LINE, [&] {
+            if (sml) return admm::sm::launch_line_inv(M, N, planes, s, spec1, last ? x_out : xg, twM);
             hipLaunchKernelGGL(g::line_inv_kernel, gl, dim3(256), lfw, s, spec1, last ? x_out : xg, twM, pM, N, T);
+            return 0;
         });
         if (rc) return rc;
         if (last) break;
@@ -663,8 +672,10 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
                 sn = tr.s + (size_t)(it - 1) * sstride;
             }
             rc = ln.run(ADMM_K_LINE, [&] {
+                if (sml) return admm::sm::launch_line_upd(M, N, planes, s, xg, so, sn, hty, spec0, twM, prm, it == 1 ? 1 : 0);
                 hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, prm,
                                    it == 1 ? 1 : 0);
+                return 0;
             });
             if (rc) return rc;
             continue;

@@ -186,7 +186,10 @@ enum {
     ADMM_OPT_GEN_TM = 4,         /* 0 (default 2048): runtime-length line block points, 256..8192        */
     ADMM_OPT_GEN_KN = 5,         /* 0 (default 1024): runtime-length column block points, 256..8192      */
     ADMM_OPT_PLANE_STAGGER = 6,  /* 0 (default): fused kernel odd-workgroup start delay, 10 ns ticks     */
-    ADMM_OPT_COUNT = 7
+    ADMM_OPT_SMOOTH = 7,         /* 1 (default): compile-time-plan kernels for the listed non-power-of-two
+                                    lengths (admm_smooth.hip); 0: runtime plans for every such shape;
+                                    2 / 3: compiled, column plans forced increasing / decreasing (sweeps)  */
+    ADMM_OPT_COUNT = 8
 };
 int admm_set_option(int option, int value);
 int admm_get_option(int option, int* value);

@@ -101,7 +101,7 @@ def test_options_roundtrip_and_validation():
     assert L.admm_set_option(99, 1) == _lib.ADMM_E_INVALID
     assert L.admm_set_option(-1, 1) == _lib.ADMM_E_INVALID
     v = ctypes.c_int(0)
-    assert L.admm_get_option(7, ctypes.byref(v)) == _lib.ADMM_E_INVALID
+    assert L.admm_get_option(len(_lib.OPTIONS), ctypes.byref(v)) == _lib.ADMM_E_INVALID
     os.environ["ADMM_FUSED"] = "0"          # the round-1 environment knob is gone
     try:
         assert _lib.get_option("FUSED") == 1

@@ -12,5 +12,5 @@ python3 -c "
 import sys; sys.path.insert(0, '$C'); import hazard_pad
 hazard_pad.compile_tu('$C/admm_capi.hip', '$O/admm_capi.o',
     ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Wno-unused-result', '-Wno-unused-value'] + sys.argv[1:])" "$@"
-hipcc --offload-arch=gfx950 -fPIC -shared -o $R/admm-deconv_amd/libadmm_deconv_$TAG.so $O/admm_capi.o $C/plane_launch.o $C/metrics_capi.o
+hipcc --offload-arch=gfx950 -fPIC -shared -o $R/admm-deconv_amd/libadmm_deconv_$TAG.so $O/admm_capi.o $C/plane_launch.o $C/admm_smooth.o $C/metrics_capi.o
 echo built $TAG

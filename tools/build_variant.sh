@@ -20,5 +20,5 @@ n = hazard_pad.compile_tu('$C/plane_launch.hip', '$O/plane_launch.o',
     ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC'] + '$NOPK'.split() + ['-mllvm', '-pragma-unroll-threshold=100000'] + sys.argv[1:])
 print('hazard pads', n)" "$@"
 fi
-hipcc --offload-arch=gfx950 -fPIC -shared -o $R/admm-deconv_amd/libadmm_deconv_$TAG.so $C/admm_capi.o $O/plane_launch.o $C/metrics_capi.o
+hipcc --offload-arch=gfx950 -fPIC -shared -o $R/admm-deconv_amd/libadmm_deconv_$TAG.so $C/admm_capi.o $O/plane_launch.o $C/admm_smooth.o $C/metrics_capi.o
 echo built $TAG
