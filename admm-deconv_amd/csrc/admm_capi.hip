@@ -625,32 +625,43 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     set_lds(g::line_upd_kernel, lup);
     set_lds(g::iso_b_kernel, lup);
     set_lds(g::column_kernel, lcol);
+    // compile-time-plan kernels where this build has the length (admm_smooth.hip): the column pass needs
+    // N, the line passes M
+    const bool smc = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(N);
+    const bool sml = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(M);
+    auto line_fwd = [&](const float* src, float2* dst) {
+        return ln.run(ADMM_K_PREP, [&] {
+            if (sml) return admm::sm::launch_line_fwd(M, N, planes, s, src, dst, twM);
+            hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, src, dst, twM, pM, N, T);
+            return 0;
+        });
+    };
     // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
-    rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, y, spec0, twM, pM, N, T); });
+    rc = line_fwd(y, spec0);
     if (rc) return rc;
     if (kh > 0) {
         rc = ln.run(ADMM_K_PREP, [&] {
+            if (smc) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 1, opt(ADMM_OPT_SMOOTH));
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 1, 1.0f);
+            return 0;
         });
         if (rc) return rc;
         rc = ln.run(ADMM_K_PREP, [&] {
+            if (sml) return admm::sm::launch_line_inv(M, N, planes, s, spec1, const_cast<float*>(hty), twM);
             hipLaunchKernelGGL(g::line_inv_kernel, gl, dim3(256), lfw, s, spec1, const_cast<float*>(hty), twM, pM, N, T);
+            return 0;
         });
         if (rc) return rc;
-        rc = ln.run(ADMM_K_PREP, [&] { hipLaunchKernelGGL(g::line_fwd_kernel, gl, dim3(256), lfw, s, hty, spec0, twM, pM, N, T); });
+        rc = line_fwd(hty, spec0);
         if (rc) return rc;
     }
     const int ng = iso_ngroups(planes);
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
-    // per-iteration kernels with compile-time plans where this build has the length (admm_smooth.hip):
-    // the column pass needs N, the line passes M
-    const bool smc = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(N);
-    const bool sml = opt(ADMM_OPT_SMOOTH) != 0 && admm::sm::has_length(M);
     for (int it = 1; it <= maxit; ++it) {
         // trajectory for h_bar: the dim-2 spectrum of iteration it before the multiply
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * planes * N * H : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            if (smc && !vsave) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, twN, 1.0f, opt(ADMM_OPT_SMOOTH));
+            if (smc && !vsave) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 0, opt(ADMM_OPT_SMOOTH));
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB,
                                vsave ? 4 : 0, 1.0f, vsave, (float*)nullptr);
             return 0;

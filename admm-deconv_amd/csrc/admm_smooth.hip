@@ -44,7 +44,7 @@ __device__ __forceinline__ float prox_w(float s, float tau) { return fabsf(s) > 
 // ---- block shapes (host and device agree through these) ---------------------------------------------
 constexpr int kNT = 256;
 #ifndef SM_UPD_U
-#define SM_UPD_U 4   // strides of loads in flight per thread in the update's elementwise phase
+#define SM_UPD_U 8   // strides of loads in flight per thread in the update's elementwise phase
 #endif
 // column blocks: KB spectral columns (a power of two, <= 16) with the LDS buffer <= 48 KiB; the
 // per-column stride FS makes the KB columns x (32 / KB) butterflies of a 32-lane group hit distinct banks
@@ -53,9 +53,15 @@ constexpr int col_fs(int NN, int KB) {
     while (fs % 32 != (32 / KB) % 32) ++fs;
     return fs;
 }
+#ifndef SM_COL_KBMAX
+#define SM_COL_KBMAX 16
+#endif
+#ifndef SM_COL_LDS_KB
+#define SM_COL_LDS_KB 48
+#endif
 constexpr int col_kb(int NN) {
-    int kb = 16;
-    while (kb > 1 && kb * col_fs(NN, kb) * 8 > 48 * 1024) kb /= 2;
+    int kb = SM_COL_KBMAX;
+    while (kb > 1 && kb * col_fs(NN, kb) * 8 > SM_COL_LDS_KB * 1024) kb /= 2;
     return kb;
 }
 // line blocks: TG lines = 2 NP (NP paired complex transforms), enough that the widest pass has about NT
@@ -69,10 +75,11 @@ constexpr int line_np() {
 }
 
 // ---- dim-2 pass --------------------------------------------------------------------------------------
-template <int NN, bool ASC>
+// MUL 0: x cs * Ct (the x-update C / (MN), ops.jl:86); 1: x Gt = conj(Sigma_c) / (MN) (H^T, PREP)
+template <int NN, bool ASC, int MUL>
 __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
-                                                     const float* __restrict__ Ct, const float2* __restrict__ twN,
-                                                     int H, float cs) {
+                                                     const float* __restrict__ Ct, const float2* __restrict__ Gt,
+                                                     const float2* __restrict__ twN, int H, float cs) {
     constexpr int KB = col_kb(NN), FS = col_fs(NN, KB);
     using S = SP<NN, ASC>;
     constexpr int P = S::P;
@@ -86,6 +93,12 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
     const float2* gs = src + po;
     float2* gd = dst + po;
     const float* cp = Ct + k0;
+    const float2* gp = Gt + k0;
+    // the multiplier of bin kj of this block's column c
+    auto mul = [&](int c, int kj, float2 v) {
+        if constexpr (MUL == 0) return cscale(v, cs * cp[(size_t)kj * H + c]);
+        else return cmul(v, gp[(size_t)kj * H + c]);
+    };
     for (int t = threadIdx.x; t < NN; t += kNT) tw[t] = twN[t];
     auto gload = [&](int c, int n) { return c < kc ? gs[(size_t)n * H + c] : make_float2(0.f, 0.f); };
     auto gstore = [&](int c, int n, float2 v) {
@@ -98,7 +111,7 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
             for (int n = 0; n < NN; ++n) v[n] = gload(c, n);
             dftR<NN, false>(v);
 #pragma unroll
-            for (int n = 0; n < NN; ++n) v[n] = cscale(v[n], cs * cp[(size_t)n * H + c]);
+            for (int n = 0; n < NN; ++n) v[n] = mul(c, n, v[n]);
             dftR<NN, true>(v);
 #pragma unroll
             for (int n = 0; n < NN; ++n) gstore(c, n, v[n]);
@@ -143,7 +156,7 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
                     dftR<R, false>(v[u]);
                     if (f < kc) {
 #pragma unroll
-                        for (int r = 0; r < R; ++r) v[u][r] = cscale(v[u][r], cs * cp[(size_t)(j + r * Q) * H + f]);
+                        for (int r = 0; r < R; ++r) v[u][r] = mul(f, j + r * Q, v[u][r]);
                     }
                     dftR<R, true>(v[u]);
 #pragma unroll
@@ -222,6 +235,42 @@ __global__ __launch_bounds__(kNT) void line_inv_kernel(const float2* __restrict_
     splan<MM, true, kNT, NP, true, MM, true, false>((T + 1) / 2, tw, A, zload, xstore);
 }
 
+// ---- dim-1 forward: real lines (y, H^T y) -> half spectra (PREP) ---------------------------------------
+// The block's T rows are contiguous: all threads load them as packed pairs (line 2p real part, 2p + 1
+// imaginary), then the FFT runs in place and the half spectra are separated (as in the update kernel).
+template <int MM>
+__global__ __launch_bounds__(kNT) void line_fwd_kernel(const float* __restrict__ src, float2* __restrict__ spec,
+                                                       const float2* __restrict__ twM, int N) {
+    constexpr int H = MM / 2 + 1, NP = line_np<MM>(), TG = 2 * NP;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* tw = reinterpret_cast<float2*>(smem_raw);
+    float2* A = tw + MM;
+    float* Af = reinterpret_cast<float*>(A);
+    const Blk b = xcd_block();
+    const int plane = b.y, j0 = b.x * TG;
+    const int T = min(TG, N - j0);
+    const float* sp = src + ((size_t)plane * N + j0) * MM;
+    for (int t = threadIdx.x; t < MM; t += kNT) tw[t] = twM[t];
+    batched<8>(T * MM, [&](int idx) { return sp[idx]; }, [&](int idx, float v) {
+        const int t = idx / MM, i = idx - t * MM;
+        Af[2 * ((t >> 1) * MM + i) + (t & 1)] = v;
+    });
+    if (T & 1)
+        for (int i = threadIdx.x; i < MM; i += kNT) A[(T >> 1) * MM + i].y = 0.0f;
+    __syncthreads();
+    const Lds<MM> al{A};
+    splan<MM, false, kNT, NP, true, MM, true, true>((T + 1) / 2, tw, A, al, al);
+    __syncthreads();
+    float2* dp = spec + ((size_t)plane * N + j0) * H;
+    for (int idx = threadIdx.x; idx < T * H; idx += kNT) {
+        const int t = idx / H, k = idx - t * H;
+        const float2* Z = A + (t >> 1) * MM;
+        const float2 z = Z[k], zm = cconj(Z[k == 0 ? 0 : MM - k]);
+        dp[idx] = (t & 1) ? make_float2(0.5f * (z.y - zm.y), -0.5f * (z.x - zm.x))
+                          : make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y + zm.y));
+    }
+}
+
 // ---- dim-1 update + forward (iterations 1 .. K-1, anisotropic) -------------------------------------
 // Phase 1, every pixel of rows j0 .. j0+T (row j0+T: the halo below, channel 0 only) in parallel with
 // batched loads: s = D x + clip(s_old), s_new stored, w = z - u (both channels) to LDS.  H^T y for the
@@ -229,10 +278,13 @@ __global__ __launch_bounds__(kNT) void line_inv_kernel(const float2* __restrict_
 // forms v = H^T y + rho D^T w for lines 2f (real part) and 2f+1 (imaginary) straight from the w rows, and
 // writes the transforms over them (all reads before a barrier).  Then the remaining passes in place, and
 // the half spectra separated: X_2p = (Z + conj Z(-k)) / 2, X_2p+1 = (Z - conj Z(-k)) / (2i).
+#ifndef SM_UPD_LDS_KB
+#define SM_UPD_LDS_KB 40
+#endif
 template <int MM>
 constexpr int upd_np() {   // paired transforms per update block: w rows (2 TG + 1) x MM floats <= 40 KiB
     int np = line_np<MM>();
-    while (np > 1 && (4 * np + 1) * MM * 4 > 40 * 1024) --np;
+    while (np > 1 && (4 * np + 1) * MM * 4 > SM_UPD_LDS_KB * 1024) --np;
     return np;
 }
 template <int MM>
@@ -421,7 +473,7 @@ static void set_lds(K kernel, size_t lds) {
 // Column plan order per length (decreasing radices unless listed): measured on MI355X with
 // tools/col_order_sweep.py (K = 25 column passes, 1 x MI355X); e.g. 250: 10 x 25 0.99 ms vs 25 x 10 1.44,
 // 480: 24 x 20 1.39 ms vs 20 x 24 1.70.  ADMM_OPT_SMOOTH = 2 / 3 force increasing / decreasing (sweeps).
-#define SM_COL_ASC_LENGTHS(X) X(250)
+#define SM_COL_ASC_LENGTHS(X) X(192) X(200) X(250) X(300) X(320) X(360) X(400) X(500) X(600) X(720) X(1200) X(2000)
 bool column_asc(int N, int mode) {
     if (mode == 2) return true;
     if (mode == 3) return false;
@@ -433,7 +485,7 @@ bool column_asc(int N, int mode) {
 }
 
 int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src, float2* dst, const float* Ct,
-                  const float2* twN, float cs, int mode) {
+                  const float2* Gt, const float2* twN, float cs, int mul, int mode) {
     const int H = M / 2 + 1;
     const bool asc = column_asc(N, mode);
 #define X(v)                                                                                               \
@@ -441,14 +493,31 @@ int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src,
         constexpr int kb = col_kb(v);                                                                      \
         const size_t lds = column_lds(v);                                                                  \
         const dim3 g((H + kb - 1) / kb, (unsigned)planes);                                                 \
-        if (asc) {                                                                                         \
-            set_lds(column_kernel<v, true>, lds);                                                          \
-            column_kernel<v, true><<<g, kNT, lds, s>>>(src, dst, Ct, twN, H, cs);                          \
+        if (mul) {                                                                                         \
+            set_lds(column_kernel<v, false, 1>, lds);                                                      \
+            column_kernel<v, false, 1><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
+        } else if (asc) {                                                                                  \
+            set_lds(column_kernel<v, true, 0>, lds);                                                       \
+            column_kernel<v, true, 0><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                   \
         } else {                                                                                           \
-            set_lds(column_kernel<v, false>, lds);                                                         \
-            column_kernel<v, false><<<g, kNT, lds, s>>>(src, dst, Ct, twN, H, cs);                         \
+            set_lds(column_kernel<v, false, 0>, lds);                                                      \
+            column_kernel<v, false, 0><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
         }                                                                                                  \
         return 0;                                                                                          \
+    }
+    SM_LENGTHS(X)
+#undef X
+    return -1;
+}
+
+int launch_line_fwd(int M, int N, size_t planes, hipStream_t s, const float* src, float2* spec, const float2* twM) {
+#define X(v)                                                                                                  \
+    if (M == v) {                                                                                             \
+        const int tg = 2 * line_np<v>();                                                                      \
+        const size_t lds = line_lds(v);                                                                       \
+        set_lds(line_fwd_kernel<v>, lds);                                                                     \
+        line_fwd_kernel<v><<<dim3((N + tg - 1) / tg, (unsigned)planes), kNT, lds, s>>>(src, spec, twM, N);   \
+        return 0;                                                                                             \
     }
     SM_LENGTHS(X)
 #undef X
