@@ -75,12 +75,27 @@ constexpr int line_np() {
 }
 
 // ---- dim-2 pass --------------------------------------------------------------------------------------
+template <int NN, bool ASC>
+struct KB_Q {
+    static constexpr int q = col_kb(NN) * SP<NN, ASC>::max_q();
+};
 // MUL 0: x cs * Ct (the x-update C / (MN), ops.jl:86); 1: x Gt = conj(Sigma_c) / (MN) (H^T, PREP)
+// threads per column block: enough for the widest pass's butterflies (KB x Q), in whole waves, <= kNT
+#ifndef SM_COL_NT_FIT
+#define SM_COL_NT_FIT 1
+#endif
+template <int NN, bool ASC>
+constexpr int col_nt() {
+    if (!SM_COL_NT_FIT) return kNT;
+    const int q = KB_Q<NN, ASC>::q;
+    const int nt = 64 * ((q + 63) / 64);
+    return nt < kNT ? nt : kNT;
+}
 template <int NN, bool ASC, int MUL>
-__global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
+__global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
                                                      const float2* __restrict__ twN, int H, float cs) {
-    constexpr int KB = col_kb(NN), FS = col_fs(NN, KB);
+    constexpr int KB = col_kb(NN), FS = col_fs(NN, KB), NT = col_nt<NN, ASC>();
     using S = SP<NN, ASC>;
     constexpr int P = S::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -99,13 +114,13 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
         if constexpr (MUL == 0) return cscale(v, cs * cp[(size_t)kj * H + c]);
         else return cmul(v, gp[(size_t)kj * H + c]);
     };
-    for (int t = threadIdx.x; t < NN; t += kNT) tw[t] = twN[t];
+    for (int t = threadIdx.x; t < NN; t += NT) tw[t] = twN[t];
     auto gload = [&](int c, int n) { return c < kc ? gs[(size_t)n * H + c] : make_float2(0.f, 0.f); };
     auto gstore = [&](int c, int n, float2 v) {
         if (c < kc) gd[(size_t)n * H + c] = v;
     };
     if constexpr (P == 1) {
-        for (int c = threadIdx.x; c < kc; c += kNT) {
+        for (int c = threadIdx.x; c < kc; c += NT) {
             float2 v[NN];
 #pragma unroll
             for (int n = 0; n < NN; ++n) v[n] = gload(c, n);
@@ -119,14 +134,14 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
     } else {
         const Lds<FS> bl{buf};
         // forward passes 0 .. P-2 (pass 0 has no twiddles: tw is ready after its barrier)
-        plan_spass<NN, 0, false, false, kNT, KB, false, false, ASC>(KB, tw, gload, bl);
+        plan_spass<NN, 0, false, false, NT, KB, false, false, ASC>(KB, tw, gload, bl);
         __syncthreads();
         if constexpr (P >= 3) {
-            plan_spass<NN, 1, false, false, kNT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 1, false, false, NT, KB, false, true, ASC>(KB, tw, bl, bl);
             __syncthreads();
         }
         if constexpr (P >= 4) {
-            plan_spass<NN, 2, false, false, kNT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 2, false, false, NT, KB, false, true, ASC>(KB, tw, bl, bl);
             __syncthreads();
         }
         // forward last pass (radix R, Ns = Q: butterfly j outputs bins j + r Q) -> x Ct -> first pass of the
@@ -134,11 +149,11 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
         {
             constexpr int R = S::template radix<false>(P - 1);
             constexpr int Q = NN / R;
-            constexpr int NR = (KB * Q + kNT - 1) / kNT;
+            constexpr int NR = (KB * Q + NT - 1) / NT;
             float2 v[NR][R];
 #pragma unroll
             for (int u = 0; u < NR; ++u) {
-                const int idx = (int)threadIdx.x + u * kNT;
+                const int idx = (int)threadIdx.x + u * NT;
                 if (idx < KB * Q) {
                     const int f = idx % KB, j = idx / KB;
 #pragma unroll
@@ -148,7 +163,7 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < NR; ++u) {
-                const int idx = (int)threadIdx.x + u * kNT;
+                const int idx = (int)threadIdx.x + u * NT;
                 if (idx < KB * Q) {
                     const int f = idx % KB, j = idx / KB;
 #pragma unroll
@@ -166,14 +181,14 @@ __global__ __launch_bounds__(kNT) void column_kernel(const float2* __restrict__ 
         }
         __syncthreads();
         if constexpr (P >= 4) {
-            plan_spass<NN, 1, true, true, kNT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 1, true, true, NT, KB, false, true, ASC>(KB, tw, bl, bl);
             __syncthreads();
         }
         if constexpr (P >= 3) {
-            plan_spass<NN, P - 2, true, true, kNT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, P - 2, true, true, NT, KB, false, true, ASC>(KB, tw, bl, bl);
             __syncthreads();
         }
-        plan_spass<NN, P - 1, true, true, kNT, KB, false, false, ASC>(KB, tw, bl, gstore);
+        plan_spass<NN, P - 1, true, true, NT, KB, false, false, ASC>(KB, tw, bl, gstore);
     }
 }
 
@@ -495,13 +510,13 @@ int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src,
         const dim3 g((H + kb - 1) / kb, (unsigned)planes);                                                 \
         if (mul) {                                                                                         \
             set_lds(column_kernel<v, false, 1>, lds);                                                      \
-            column_kernel<v, false, 1><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
+            column_kernel<v, false, 1><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
         } else if (asc) {                                                                                  \
             set_lds(column_kernel<v, true, 0>, lds);                                                       \
-            column_kernel<v, true, 0><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                   \
+            column_kernel<v, true, 0><<<g, col_nt<v, true>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                   \
         } else {                                                                                           \
             set_lds(column_kernel<v, false, 0>, lds);                                                      \
-            column_kernel<v, false, 0><<<g, kNT, lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
+            column_kernel<v, false, 0><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
         }                                                                                                  \
         return 0;                                                                                          \
     }
