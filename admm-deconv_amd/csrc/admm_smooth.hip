@@ -43,6 +43,9 @@ __device__ __forceinline__ float prox_w(float s, float tau) { return fabsf(s) > 
 
 // ---- block shapes (host and device agree through these) ---------------------------------------------
 constexpr int kNT = 256;
+// radix caps: line transforms 16 (more passes but fewer live registers: 250^2 line passes 3.21 -> 2.95 ms
+// per solve, 480 x 640 3.90 -> 3.63), column transforms 32 (a smaller cap did not help them)
+constexpr int kLineR = 16, kColR = 32;
 #ifndef SM_UPD_U
 #define SM_UPD_U 8   // strides of loads in flight per thread in the update's elementwise phase
 #endif
@@ -68,7 +71,7 @@ constexpr int col_kb(int NN) {
 // butterflies, at most 16 lines and 32 KiB of transform buffer
 template <int MM>
 constexpr int line_np() {
-    int np = (kNT + SP<MM, true>::max_q() - 1) / SP<MM, true>::max_q();
+    int np = (kNT + SP<MM, true, kLineR>::max_q() - 1) / SP<MM, true, kLineR>::max_q();
     if (np > 8) np = 8;
     while (np > 1 && np * MM * 8 > 32 * 1024) --np;
     return np;
@@ -77,7 +80,7 @@ constexpr int line_np() {
 // ---- dim-2 pass --------------------------------------------------------------------------------------
 template <int NN, bool ASC>
 struct KB_Q {
-    static constexpr int q = col_kb(NN) * SP<NN, ASC>::max_q();
+    static constexpr int q = col_kb(NN) * SP<NN, ASC, kColR>::max_q();
 };
 // MUL 0: x cs * Ct (the x-update C / (MN), ops.jl:86); 1: x Gt = conj(Sigma_c) / (MN) (H^T, PREP)
 // threads per column block: enough for the widest pass's butterflies (KB x Q), in whole waves, <= kNT
@@ -96,7 +99,7 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
                                                      const float2* __restrict__ twN, int H, float cs) {
     constexpr int KB = col_kb(NN), FS = col_fs(NN, KB), NT = col_nt<NN, ASC>();
-    using S = SP<NN, ASC>;
+    using S = SP<NN, ASC, kColR>;
     constexpr int P = S::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
@@ -134,14 +137,14 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
     } else {
         const Lds<FS> bl{buf};
         // forward passes 0 .. P-2 (pass 0 has no twiddles: tw is ready after its barrier)
-        plan_spass<NN, 0, false, false, NT, KB, false, false, ASC>(KB, tw, gload, bl);
+        plan_spass<NN, 0, false, false, NT, KB, false, false, ASC, kColR>(KB, tw, gload, bl);
         __syncthreads();
         if constexpr (P >= 3) {
-            plan_spass<NN, 1, false, false, NT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 1, false, false, NT, KB, false, true, ASC, kColR>(KB, tw, bl, bl);
             __syncthreads();
         }
         if constexpr (P >= 4) {
-            plan_spass<NN, 2, false, false, NT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 2, false, false, NT, KB, false, true, ASC, kColR>(KB, tw, bl, bl);
             __syncthreads();
         }
         // forward last pass (radix R, Ns = Q: butterfly j outputs bins j + r Q) -> x Ct -> first pass of the
@@ -181,14 +184,14 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
         }
         __syncthreads();
         if constexpr (P >= 4) {
-            plan_spass<NN, 1, true, true, NT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, 1, true, true, NT, KB, false, true, ASC, kColR>(KB, tw, bl, bl);
             __syncthreads();
         }
         if constexpr (P >= 3) {
-            plan_spass<NN, P - 2, true, true, NT, KB, false, true, ASC>(KB, tw, bl, bl);
+            plan_spass<NN, P - 2, true, true, NT, KB, false, true, ASC, kColR>(KB, tw, bl, bl);
             __syncthreads();
         }
-        plan_spass<NN, P - 1, true, true, NT, KB, false, false, ASC>(KB, tw, bl, gstore);
+        plan_spass<NN, P - 1, true, true, NT, KB, false, false, ASC, kColR>(KB, tw, bl, gstore);
     }
 }
 
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(kNT) void line_inv_kernel(const float2* __restrict_
         dp[(size_t)(2 * f) * MM + n] = v.x;
         if (2 * f + 1 < T) dp[(size_t)(2 * f + 1) * MM + n] = v.y;
     };
-    splan<MM, true, kNT, NP, true, MM, true, false>((T + 1) / 2, tw, A, zload, xstore);
+    splan<MM, true, kNT, NP, true, MM, true, false, true, kLineR>((T + 1) / 2, tw, A, zload, xstore);
 }
 
 // ---- dim-1 forward: real lines (y, H^T y) -> half spectra (PREP) ---------------------------------------
@@ -274,7 +277,7 @@ __global__ __launch_bounds__(kNT) void line_fwd_kernel(const float* __restrict__
         for (int i = threadIdx.x; i < MM; i += kNT) A[(T >> 1) * MM + i].y = 0.0f;
     __syncthreads();
     const Lds<MM> al{A};
-    splan<MM, false, kNT, NP, true, MM, true, true>((T + 1) / 2, tw, A, al, al);
+    splan<MM, false, kNT, NP, true, MM, true, true, true, kLineR>((T + 1) / 2, tw, A, al, al);
     __syncthreads();
     float2* dp = spec + ((size_t)plane * N + j0) * H;
     for (int idx = threadIdx.x; idx < T * H; idx += kNT) {
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(kNT) void line_upd_kernel(const float* __restrict__
                                                        float2* __restrict__ spec, const float2* __restrict__ twM,
                                                        int N, const float* __restrict__ prm, int first) {
     constexpr int H = MM / 2 + 1, NP = upd_np<MM>(), TG = 2 * NP;
-    using S = SP<MM, true>;
+    using S = SP<MM, true, kLineR>;
     constexpr int P = S::P;
     constexpr int R0 = S::template radix<false>(0), Q0 = MM / R0;
     constexpr int NR0 = (NP * Q0 + kNT - 1) / kNT;
@@ -411,15 +414,15 @@ __global__ __launch_bounds__(kNT) void line_upd_kernel(const float* __restrict__
     __syncthreads();
     const Lds<MM> al{A};
     if constexpr (P >= 3) {
-        plan_spass<MM, 1, false, false, kNT, NP, true, true, true>(np, tw, al, al);
+        plan_spass<MM, 1, false, false, kNT, NP, true, true, true, kLineR>(np, tw, al, al);
         __syncthreads();
     }
     if constexpr (P >= 4) {
-        plan_spass<MM, 2, false, false, kNT, NP, true, true, true>(np, tw, al, al);
+        plan_spass<MM, 2, false, false, kNT, NP, true, true, true, kLineR>(np, tw, al, al);
         __syncthreads();
     }
     if constexpr (P >= 2) {
-        plan_spass<MM, P - 1, false, false, kNT, NP, true, true, true>(np, tw, al, al);
+        plan_spass<MM, P - 1, false, false, kNT, NP, true, true, true, kLineR>(np, tw, al, al);
         __syncthreads();
     }
     float2* dp = spec + ((size_t)plane * N + j0) * H;

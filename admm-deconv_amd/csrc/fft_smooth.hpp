@@ -3,8 +3,9 @@
 // The reference transforms any M x N (FFTW / CUFFT plans, /root/reference/src/ops/ops.jl:26,35-36,86 and
 // :108,117-118,168).  admm_generic.hip covers every length with runtime plans; this header gives lengths
 // whose prime factors are all <= 31 a plan fixed at compile time:
-//   * a transform of LEN points is P <= 4 Stockham passes of radix <= 32 (make_splan: fewest passes,
-//     then the smallest largest radix; 250 = 25 x 10, 480 = 24 x 20, 640 = 32 x 20, 2048 = 16 x 16 x 8);
+//   * a transform of LEN points is P <= 4 Stockham passes of radix <= MAXR (make_splan: fewest passes,
+//     then the smallest largest radix; radix <= 32: 250 = 25 x 10, 480 = 24 x 20, 640 = 32 x 20;
+//     <= 16: 250 = 10 x 5 x 5, 640 = 16 x 8 x 5);
 //   * each radix-R butterfly runs in registers: R in {2, 4, 8, 16} as in fft_reg.hpp, odd primes by the
 //     symmetric direct form, composite R as A x (R/A) Cooley-Tukey with compile-time twiddles;
 //   * pass p maps src[j + r LEN/R] -> dst[(j / Ns) Ns R + j % Ns + r Ns] after the twiddle
@@ -175,25 +176,25 @@ __device__ __forceinline__ void dftR(float2 (&v)[R]) {
 }
 
 // ---- plans -------------------------------------------------------------------------------------------
-constexpr int kMaxRadix = 32;
+constexpr int kMaxRadix = 32;   // largest in-register DFT
 struct SPlan {
     int P;
     int r[4];
 };
 constexpr int imax(int a, int b) { return a > b ? a : b; }
 constexpr int imin(int a, int b) { return a < b ? a : b; }
-// the best plan of n into exactly `passes` radices <= kMaxRadix (smallest largest radix; radices in
+// the best plan of n into exactly `passes` radices <= maxr (smallest largest radix; radices in
 // non-increasing order); P = 0 if there is none
-constexpr SPlan plan_exact(int n, int passes) {
+constexpr SPlan plan_exact(int n, int passes, int maxr) {
     SPlan best{0, {1, 1, 1, 1}};
     if (passes == 1) {
-        if (n >= 2 && n <= kMaxRadix) best = SPlan{1, {n, 1, 1, 1}};
+        if (n >= 2 && n <= maxr) best = SPlan{1, {n, 1, 1, 1}};
         return best;
     }
     int best_max = 1 << 30;
-    for (int a = 2; a <= kMaxRadix; ++a) {
+    for (int a = 2; a <= maxr; ++a) {
         if (n % a) continue;
-        const SPlan sub = plan_exact(n / a, passes - 1);
+        const SPlan sub = plan_exact(n / a, passes - 1, maxr);
         if (!sub.P || sub.r[0] > a) continue;   // keep radices non-increasing (one canonical order)
         const int mx = a;
         if (mx < best_max) {
@@ -205,9 +206,9 @@ constexpr SPlan plan_exact(int n, int passes) {
 }
 // ASC: radices in increasing order (the first pass has the most butterflies and the fewest registers per
 // butterfly: the line kernels' choice); otherwise decreasing (the column kernel's)
-constexpr SPlan make_splan(int n, bool asc) {
+constexpr SPlan make_splan(int n, bool asc, int maxr) {
     for (int p = 1; p <= 4; ++p) {
-        SPlan s = plan_exact(n, p);
+        SPlan s = plan_exact(n, p, maxr);
         if (s.P) {
             if (asc)
                 for (int a = 0, b = s.P - 1; a < b; ++a, --b) {
@@ -220,9 +221,10 @@ constexpr SPlan make_splan(int n, bool asc) {
     }
     return SPlan{0, {1, 1, 1, 1}};
 }
-template <int LEN, bool ASC = false>
+// MAXR: radix cap (more passes, fewer live registers per butterfly when smaller)
+template <int LEN, bool ASC = false, int MAXR = kMaxRadix>
 struct SP {
-    static constexpr SPlan pl = make_splan(LEN, ASC);
+    static constexpr SPlan pl = make_splan(LEN, ASC, MAXR);
     static constexpr int P = pl.P;
     static_assert(P >= 1, "length has no plan (a prime factor > 31, or > 32^4)");
     // radix of pass p (REV: the plan run backwards) and the span Ns before it
@@ -290,10 +292,10 @@ __device__ __forceinline__ void spass(int cnt, const float2* __restrict__ tw, Lo
 }
 
 // pass p of the plan of LEN (REV: reversed plan; ASC: the increasing-radix plan)
-template <int LEN, int p, bool REV, bool INV, int NT, int CNTMAX, bool FMAJ, bool INPLACE, bool ASC = false, class Load,
-          class Store>
+template <int LEN, int p, bool REV, bool INV, int NT, int CNTMAX, bool FMAJ, bool INPLACE, bool ASC = false,
+          int MAXR = kMaxRadix, class Load, class Store>
 __device__ __forceinline__ void plan_spass(int cnt, const float2* __restrict__ tw, Load&& ld, Store&& st) {
-    using S = SP<LEN, ASC>;
+    using S = SP<LEN, ASC, MAXR>;
     spass<LEN, S::template radix<REV>(p), S::template ns<REV>(p), INV, NT, CNTMAX, FMAJ, INPLACE>(cnt, tw, ld, st);
 }
 
@@ -308,25 +310,25 @@ struct Lds {
 // A whole plan, in place in one LDS buffer between the first pass (reads through ld) and the last
 // (writes through st).  Barriers between passes; the caller places the ones before and after.
 // IN0: ld reads the buffer itself (the first pass is then in place); INL: st writes the buffer.
-template <int LEN, bool INV, int NT, int CNTMAX, bool FMAJ, int FS, bool IN0, bool INL, bool ASC = true, class Load,
-          class Store>
+template <int LEN, bool INV, int NT, int CNTMAX, bool FMAJ, int FS, bool IN0, bool INL, bool ASC = true,
+          int MAXR = kMaxRadix, class Load, class Store>
 __device__ __forceinline__ void splan(int cnt, const float2* __restrict__ tw, float2* buf, Load&& ld, Store&& st) {
-    constexpr int P = SP<LEN, ASC>::P;
+    constexpr int P = SP<LEN, ASC, MAXR>::P;
     const Lds<FS> b{buf};
     if constexpr (P == 1) {
-        plan_spass<LEN, 0, false, INV, NT, CNTMAX, FMAJ, IN0 && INL, ASC>(cnt, tw, ld, st);
+        plan_spass<LEN, 0, false, INV, NT, CNTMAX, FMAJ, IN0 && INL, ASC, MAXR>(cnt, tw, ld, st);
     } else {
-        plan_spass<LEN, 0, false, INV, NT, CNTMAX, FMAJ, IN0, ASC>(cnt, tw, ld, b);
+        plan_spass<LEN, 0, false, INV, NT, CNTMAX, FMAJ, IN0, ASC, MAXR>(cnt, tw, ld, b);
         __syncthreads();
         if constexpr (P >= 3) {
-            plan_spass<LEN, 1, false, INV, NT, CNTMAX, FMAJ, true, ASC>(cnt, tw, b, b);
+            plan_spass<LEN, 1, false, INV, NT, CNTMAX, FMAJ, true, ASC, MAXR>(cnt, tw, b, b);
             __syncthreads();
         }
         if constexpr (P >= 4) {
-            plan_spass<LEN, 2, false, INV, NT, CNTMAX, FMAJ, true, ASC>(cnt, tw, b, b);
+            plan_spass<LEN, 2, false, INV, NT, CNTMAX, FMAJ, true, ASC, MAXR>(cnt, tw, b, b);
             __syncthreads();
         }
-        plan_spass<LEN, P - 1, false, INV, NT, CNTMAX, FMAJ, INL, ASC>(cnt, tw, b, st);
+        plan_spass<LEN, P - 1, false, INV, NT, CNTMAX, FMAJ, INL, ASC, MAXR>(cnt, tw, b, st);
     }
 }
 
