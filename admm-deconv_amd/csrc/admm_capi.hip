@@ -13,6 +13,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
@@ -365,6 +366,13 @@ int check_shape(int M, int N, int P, int B, int kh, int kw, int iso) {
     return ADMM_OK;
 }
 
+// Planes per launch sequence.  The 2-pass kernels index planes by blockIdx.y (<= 65535), so a larger
+// anisotropic forward runs as consecutive chunks of this many planes through one chunk-sized workspace
+// (planes are independent, ops.jl:168-173).  A multiple of 256: every chunk but the last fills whole
+// waves of the fused kernel (one workgroup per CU).
+constexpr size_t kChunkPlanes = 255 * 256;
+size_t launch_planes(size_t planes) { return planes < kChunkPlanes ? planes : kChunkPlanes; }
+
 }  // namespace
 
 extern "C" {
@@ -377,7 +385,7 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    *out_bytes = make_layout(M, N, (size_t)P * B, kh > 0, iso != 0).total;
+    *out_bytes = make_layout(M, N, launch_planes((size_t)P * B), kh > 0, iso != 0).total;
     return ADMM_OK;
 }
 
@@ -923,14 +931,16 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rc = check_common(y, x_out, maxit);
     if (rc) return rc;
     const size_t planes = (size_t)P * B;
-    if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
-    const Layout lay = make_layout(M, N, planes, kh > 0, iso != 0);
+    const size_t chunk = launch_planes(planes);   // check_shape kept iso batches to one chunk
+    const Layout lay = make_layout(M, N, chunk, kh > 0, iso != 0);
     rc = check_ws(workspace, workspace_bytes, lay.total);
     if (rc) return rc;
     rec_forget(workspace);   // whatever was recorded there is overwritten now
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
-    rc = run_forward(ln, y, x_out, M, N, planes, h, kh, kw, sc, iso, maxit, static_cast<unsigned char*>(workspace), lay,
-                     Traj{}, red);
+    const size_t MN = (size_t)M * N;
+    for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
+        rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
+                         maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red);
     int rc2 = ln.finish();
     return rc ? rc : rc2;
 }
@@ -951,7 +961,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     if ((phases & 2) && (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)))
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
-    if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "at most 65535 planes per call (split the batch)");
+    if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
     const bool want_h = (phases == 1 ? want_hbar_rec != 0 : h_bar != nullptr) && kh > 0;
     // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
     const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
@@ -1275,6 +1285,7 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
+    if ((size_t)P * B > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
     *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
     return ADMM_OK;
 }

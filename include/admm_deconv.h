@@ -73,7 +73,11 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
  * arrays: returns x after `maxit` ADMM iterations of
  *   x = irfft(C .* rfft(H^T y + ρ D^T(z-u))),  z = prox(Dx+u, λ/ρ),  u = u + Dx - z
  * with prox = ST (iso == 0, ops.jl:9) or BT (iso == 1, ops.jl:10; couples the whole batch).
- * maxit == 0 returns zeros (the reference's initial x, ops.jl:46). */
+ * maxit == 0 returns zeros (the reference's initial x, ops.jl:46).
+ * Batch size: iso == 1 takes at most 65535 planes (P*B) per call.  iso == 0 takes any number; above
+ * 65,280 planes the library solves consecutive chunks of 65,280 planes through one chunk-sized
+ * workspace (admm_tvd_workspace_bytes sizes it).  The adjoint entry points below take at most 65535
+ * planes per call. */
 int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int B,
                          const float* h, int kh, int kw, float lambda, float rho, int iso,
                          int maxit, void* workspace, size_t workspace_bytes, void* stream);

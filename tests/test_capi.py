@@ -39,6 +39,20 @@ def test_workspace_bytes():
     assert _lib.workspace_bytes(256, 256, 1, 512, 15, 15, True) > n1
 
 
+def test_workspace_sized_for_one_chunk_of_planes():
+    """Aniso batches above 65,280 planes run as consecutive chunks through one chunk-sized workspace
+    (include/admm_deconv.h); iso (batch-coupled) and the adjoint keep the 65535-plane limit."""
+    chunk = 255 * 256
+    assert _lib.workspace_bytes(8, 8, 1, 200000, 3, 3, False) == _lib.workspace_bytes(8, 8, 1, chunk, 3, 3, False)
+    assert _lib.workspace_bytes(8, 8, 1, chunk, 3, 3, False) > _lib.workspace_bytes(8, 8, 1, chunk - 256, 3, 3, False)
+    out = ctypes.c_size_t(0)
+    L = _lib.load()
+    assert L.admm_tvd_workspace_bytes(8, 8, 1, 70000, 3, 3, 1, ctypes.byref(out)) == _lib.ADMM_E_UNSUPPORTED
+    assert L.admm_tvd_backward_workspace_bytes(8, 8, 1, 70000, 3, 3, 0, 5, 0, ctypes.byref(out)) == \
+        _lib.ADMM_E_UNSUPPORTED
+    assert "65535" in L.admm_last_error().decode()
+
+
 @pytest.mark.parametrize("args,code", [
     ((8192, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # M too large
     ((64, 8192, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large

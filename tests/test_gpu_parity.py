@@ -125,6 +125,27 @@ def test_batch_sharding_invariance(dev):
     assert torch.equal(full, part)
 
 
+@pytest.mark.parametrize("M,N", [(8, 8), (6, 5)], ids=["pow2-8x8", "generic-6x5"])
+def test_forward_more_planes_than_one_launch(dev, M, N):
+    """Above 65,280 planes the aniso forward runs consecutive plane chunks (admm_capi.hip kChunkPlanes):
+    bitwise the same planes as two calls that each fit one launch sequence."""
+    rng = np.random.default_rng(7)
+    B = 70000
+    y = torch.from_numpy(rng.random((B, 1, N, M), dtype=np.float32)).to(dev)
+    ht = torch.from_numpy(synth.gaussian_psf(3, 0.8)).to(dev)
+    full = admm_deconv.tvd_fft(y, 0.01, 0.05, ht, False, 5)
+    cut = 35000   # keeps the second half 16-byte aligned for odd M x N
+    part = torch.cat([admm_deconv.tvd_fft(y[:cut].contiguous(), 0.01, 0.05, ht, False, 5),
+                      admm_deconv.tvd_fft(y[cut:].contiguous(), 0.01, 0.05, ht, False, 5)])
+    torch.cuda.synchronize()
+    assert torch.equal(full, part)
+    ref = run_gpu(dev, y[-3:].cpu().numpy(), 0.01, 0.05, synth.gaussian_psf(3, 0.8), False, 5)
+    assert np.array_equal(full[-3:].cpu().numpy(), ref)
+    tail = y[-2:].cpu().numpy()
+    assert_parity(full[-2:].cpu().numpy(), run_oracle(tail, 0.01, 0.05, synth.gaussian_psf(3, 0.8), False, 5),
+                  what=f"chunked {M}x{N}")
+
+
 ISO_CASES = [
     # (B, P, N, M, psf, lam, rho, K)
     (4, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 10),
