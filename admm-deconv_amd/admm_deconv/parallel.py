@@ -62,9 +62,19 @@ class ShardGather:
     CUDA slices going through host copies.
 
     `gathered()` returns rank dst's (world * B_local, ...) result of the last step (None elsewhere);
-    call it after the device work has completed (torch.cuda.synchronize or `wait()`)."""
+    call it after the device work has completed (torch.cuda.synchronize or `wait()`).
 
-    def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0):
+    engine="ipc" moves the outputs without any collective kernel: rank dst shares its receive buffer
+    once through a HIP IPC handle, and every rank copies each solved slice into its part of it with an
+    async device copy on the second stream.  The HIP runtime hands peer copies of >= ROC_P2P_SDMA_SIZE
+    to the SDMA engines, so no CU is held while the bytes cross xGMI.  An RCCL gather keeps kernel blocks
+    resident for the whole transfer, and the fused solve needs every CU: one such block costs it
+    ~0.8 ms per 1.2 ms (tools/contend.py).  With ipc the receive buffer is complete once
+    every rank has finished its copies, i.e. after `wait()`, a device synchronize and a barrier on all
+    ranks.  If any rank cannot open the handle, every rank falls back to engine "rccl" (`self.engine`
+    says which ran)."""
+
+    def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0, engine="rccl"):
         self.y = y_local
         self.solve = solve
         self.group = group
@@ -77,8 +87,13 @@ class ShardGather:
         self.out = [torch.empty_like(y_local) for _ in range(2)]
         self.cuda = y_local.is_cuda
         self.gloo = self.world > 1 and dist.get_backend(group) == "gloo"
-        self.async_comm = self.cuda and self.world > 1 and not self.gloo
-        if self.world > 1 and self.rank == dst:
+        self.engine = "rccl"
+        if engine == "ipc" and self.cuda and self.world > 1:
+            self.engine = "ipc" if self._ipc_setup(y_local) else "rccl"
+        self.async_comm = self.cuda and self.world > 1 and (not self.gloo or self.engine == "ipc")
+        if self.engine == "ipc":
+            pass   # self.recv (rank dst) / self.remote (others) set by _ipc_setup
+        elif self.world > 1 and self.rank == dst:
             full = (self.world * n,) + tuple(y_local.shape[1:])
             dev = "cpu" if self.gloo else y_local.device
             self.recv = torch.empty(full, dtype=y_local.dtype, device=dev)
@@ -88,6 +103,46 @@ class ShardGather:
             self.comm = torch.cuda.Stream(device=y_local.device)
             self.freed = [None, None]      # event: the gathers reading out[b] have completed
         self.i = 0
+
+    def _ipc_setup(self, y_local):
+        """Rank dst allocates the receive buffer and shares its IPC handle; the others open it.  Returns
+        whether every rank succeeded (a collective: all ranks agree)."""
+        from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
+        n = y_local.shape[0]
+        full = (self.world * n,) + tuple(y_local.shape[1:])
+        ok = 1
+        self.recv, self.remote = None, None
+        obj = [None]
+        try:
+            if self.rank == self.dst:
+                self.recv = torch.empty(full, dtype=y_local.dtype, device=y_local.device)
+                obj = [reduce_tensor(self.recv)[1]]
+        except Exception:   # noqa: BLE001 -- any failure selects the RCCL path on every rank
+            ok = 0
+        dist.broadcast_object_list(obj, src=self.dst, group=self.group)
+        try:
+            if self.rank != self.dst:
+                if obj[0] is None:
+                    raise RuntimeError("no handle")
+                self.remote = rebuild_cuda_tensor(*obj[0])
+                if tuple(self.remote.shape) != full:
+                    raise RuntimeError("shape mismatch")
+        except Exception:   # noqa: BLE001
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device="cpu" if self.gloo else y_local.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 1:
+            return True
+        self.recv, self.remote = None, None
+        return False
+
+    def _out(self, b):
+        """Output buffer b of this rank.  With ipc, rank dst solves straight into its own part of the
+        receive buffer (nothing reads it during the steps), so it copies nothing."""
+        if self.engine == "ipc" and self.rank == self.dst:
+            n = self.y.shape[0]
+            return self.recv[self.rank * n: (self.rank + 1) * n]
+        return self.out[b]
 
     def _parts(self, c):
         """rank dst's receive views for chunk c of every rank (rank r's chunk lands at r * n + start)."""
@@ -99,19 +154,23 @@ class ShardGather:
 
     def step(self):
         b = self.i & 1
-        out = self.out[b]
+        out = self._out(b)
         if self.async_comm and self.freed[b] is not None:
             torch.cuda.current_stream(self.y.device).wait_event(self.freed[b])
         for c, (s, k) in enumerate(self.bounds):
             self.solve(self.y[s:s + k], out[s:s + k])
-            if self.world == 1:
+            if self.world == 1 or (self.engine == "ipc" and self.rank == self.dst):
                 continue
             if self.async_comm:
                 done = torch.cuda.Event()
                 done.record(torch.cuda.current_stream(self.y.device))
                 with torch.cuda.stream(self.comm):
                     self.comm.wait_event(done)
-                    dist.gather(out[s:s + k], self._parts(c), dst=self.dst, group=self.group)
+                    if self.engine == "ipc":
+                        n = self.y.shape[0]
+                        self.remote[self.rank * n + s: self.rank * n + s + k].copy_(out[s:s + k], non_blocking=True)
+                    else:
+                        dist.gather(out[s:s + k], self._parts(c), dst=self.dst, group=self.group)
             else:
                 src = out[s:s + k].cpu() if (self.gloo and self.cuda) else out[s:s + k]
                 dist.gather(src, self._parts(c), dst=self.dst, group=self.group)
@@ -128,7 +187,7 @@ class ShardGather:
 
     def local(self):
         """This rank's solved shard from the last step."""
-        return self.out[(self.i - 1) & 1]
+        return self._out((self.i - 1) & 1)
 
     def gathered(self):
         if self.world == 1:

@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's; c3 -> 2048/N)")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the gather to rank 0 (solve only)")
     ap.add_argument("--chunks", type=int, default=1, help="N > 1: slices per shard, each gathered as soon as solved")
+    ap.add_argument("--gather-engine", default="ipc", choices=("ipc", "rccl"),
+                    help="N > 1: 'ipc' = every rank copies its solved slices into rank 0's IPC-shared receive buffer "
+                         "(async peer copies, SDMA: no CU held); 'rccl' = dist.gather over RCCL (falls back to it "
+                         "when the IPC handle cannot be opened)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: nccl (RCCL over xGMI); gloo only to rehearse the schedule with ranks sharing a GPU")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -306,7 +310,7 @@ def main():
         i = chunk_of.setdefault(ys.data_ptr(), len(chunk_of) % len(ws))
         admm_deconv.tvd_fft(ys, synth.LAMBDA, synth.RHO, h, False, K, out=xs, workspace=ws[i], stream=stream)
 
-    sg = parallel.ShardGather(y, solve, chunks=args.chunks) if gather else None
+    sg = parallel.ShardGather(y, solve, chunks=args.chunks, engine=args.gather_engine) if gather else None
 
     def step():
         if sg is not None:
@@ -394,7 +398,8 @@ def main():
                                    f"Gaussian PSF (sigma {cfg['psf'][1]}), K={K}, anisotropic TV, lambda {synth.LAMBDA}, "
                                    f"rho {synth.RHO}", "global_batch": B * world, "image": [M, N, P], "K": K,
                        "parallelism": f"batch-shard x{world}" + (
-                           (" + RCCL gather" if args.backend == "nccl" else " + gloo gather") + " (overlapped, "
+                           (" + IPC push gather (async peer copies over xGMI)" if sg.engine == "ipc" else
+                            " + RCCL gather" if args.backend == "nccl" else " + gloo gather") + " (overlapped, "
                            f"{args.chunks} chunk{'s' if args.chunks > 1 else ''}/shard)" if gather else "")},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -31,7 +31,7 @@ def _batch(case, n, g0=0):
     return synth.make_batch(n, M, N, h, g0=g0), h
 
 
-def _worker(rank, world, port, q, case, n_local, chunks):
+def _worker(rank, world, port, q, case, n_local, chunks, engine):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
@@ -43,12 +43,13 @@ def _worker(rank, world, port, q, case, n_local, chunks):
     def solve(ys, xs):
         admm_deconv.tvd_fft(ys, LAM, RHO, ht, False, K, out=xs, workspace=ws)
 
-    sg = parallel.ShardGather(yt, solve, chunks=chunks)
+    sg = parallel.ShardGather(yt, solve, chunks=chunks, engine=engine)
     sg.step()
     sg.step()
     sg.wait()
     torch.cuda.synchronize()
-    q.put((rank, None if rank else sg.gathered().numpy().copy(), sg.local().cpu().numpy()))
+    dist.barrier()   # ipc: rank 0's buffer is complete once every rank's copies have finished
+    q.put((rank, None if rank else sg.gathered().cpu().numpy().copy(), sg.local().cpu().numpy(), sg.engine))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,8 +62,11 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("case,chunks", [("fused", 1), ("fused", 2), ("2pass", 2)])
-def test_aniso_shard_gather_two_processes(dev, case, chunks):
+@pytest.mark.parametrize("case,chunks,engine", [("fused", 1, "rccl"), ("fused", 2, "rccl"), ("2pass", 2, "rccl"),
+                                                ("fused", 1, "ipc"), ("fused", 2, "ipc"), ("2pass", 3, "ipc")])
+def test_aniso_shard_gather_two_processes(dev, case, chunks, engine):
+    """engine "rccl" runs dist.gather (here gloo); "ipc" copies every solved slice into rank 0's receive
+    buffer opened through a HIP IPC handle (on this box both ranks share the one GPU)."""
     world, n_local = 2, 3
     y, h = _batch(case, world * n_local)
     ref = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), LAM, RHO, torch.from_numpy(h).to(dev), False, K)
@@ -70,13 +74,15 @@ def test_aniso_shard_gather_two_processes(dev, case, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case, n_local, chunks)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case, n_local, chunks, engine))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    assert all(r[3] == engine for r in res), [r[3] for r in res]   # no silent fallback
     assert np.array_equal(res[0][1], ref)
     for r in range(world):
         assert np.array_equal(res[r][2], ref[r * n_local:(r + 1) * n_local])
@@ -95,4 +101,4 @@ def test_bench_two_ranks_gloo(dev):
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 16
-    assert "gather" in d["config"]["parallelism"] and d["value"] > 0
+    assert "IPC push gather" in d["config"]["parallelism"] and d["value"] > 0
