@@ -127,6 +127,10 @@ class ShardGather:
                 self.remote = rebuild_cuda_tensor(*obj[0])
                 if tuple(self.remote.shape) != full:
                     raise RuntimeError("shape mismatch")
+                # one real copy through the path the steps use (peer access, engine choice): any error
+                # here selects RCCL instead of failing mid-run; the slice is overwritten by the first step
+                self.remote[self.rank * n: self.rank * n + 1].copy_(y_local[:1])
+                torch.cuda.synchronize(y_local.device)
         except Exception:   # noqa: BLE001
             ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device="cpu" if self.gloo else y_local.device)
