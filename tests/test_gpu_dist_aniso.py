@@ -62,12 +62,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("case,chunks,engine", [("fused", 1, "rccl"), ("fused", 2, "rccl"), ("2pass", 2, "rccl"),
-                                                ("fused", 1, "ipc"), ("fused", 2, "ipc"), ("2pass", 3, "ipc")])
-def test_aniso_shard_gather_two_processes(dev, case, chunks, engine):
+@pytest.mark.parametrize("case,chunks,engine,world", [
+    ("fused", 1, "rccl", 2), ("fused", 2, "rccl", 2), ("2pass", 2, "rccl", 2),
+    ("fused", 1, "ipc", 2), ("fused", 2, "ipc", 2), ("2pass", 3, "ipc", 2), ("2pass", 2, "ipc", 4)])
+def test_aniso_shard_gather_two_processes(dev, case, chunks, engine, world):
     """engine "rccl" runs dist.gather (here gloo); "ipc" copies every solved slice into rank 0's receive
-    buffer opened through a HIP IPC handle (on this box both ranks share the one GPU)."""
-    world, n_local = 2, 3
+    buffer opened through a HIP IPC handle (on this box all ranks share the one GPU; 4 ranks = 3 peers
+    writing into one shared buffer)."""
+    n_local = 3
     y, h = _batch(case, world * n_local)
     ref = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), LAM, RHO, torch.from_numpy(h).to(dev), False, K)
     ref = ref.cpu().numpy()
