@@ -236,11 +236,13 @@ def _scalars_for(lam, rho, device, stream):
     return None, _scalar(lam, "lambda"), _scalar(rho, "rho")
 
 
-def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, workspace=None,
-                     stream=None, group=None):
+def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, need_y=True,
+                     workspace=None, stream=None, group=None):
     """Adjoint of tvd_fft through all `maxit` unrolled iterations (what Zygote computes for the
     reference, src/train.jl:51).  Returns (x, y_bar, h_bar, lam_bar, rho_bar); h_bar is None without a PSF
-    or when need_h is False.  Recomputes the forward (x is returned for convenience).
+    or when need_h is False; y_bar is None when need_y is False (the sweep then keeps no running sum of
+    vbar unless h_bar needs it: 8 B/px less traffic per reverse step).  Recomputes the forward (x is
+    returned for convenience).
     With `group` (isotropic prox, batch sharded over the group's ranks) h_bar / lam_bar / rho_bar are
     this shard's contributions: their sum over ranks is the gradient of the whole batch."""
     shape, y4, hb = _prep(y, h)
@@ -255,10 +257,10 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
         workspace = _default_workspace("bwd", y.device, stream)
     ws_ptr, ws_len = workspace.get(nbytes, y.device, stream)
     x = torch.empty_like(y4)
-    y_bar = torch.empty_like(y4)
+    y_bar = torch.empty_like(y4) if need_y else None
     h_bar = torch.empty_like(hb) if want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y.device)
-    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if want_h else None, scal.data_ptr(),
+    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr() if need_y else None, h_bar.data_ptr() if want_h else None, scal.data_ptr(),
             scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
     tail = (int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle)
     red, keep = _make_reducer(workspace, group) if _sharded(isotropic, group) else (None, None)
@@ -270,7 +272,7 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     else:
         _lib.check(L.admm_tvd_backward_f32(*head, lam_h, rho_h, *tail))
     del keep
-    return x.reshape(shape), y_bar.reshape(shape), h_bar, scal[0], scal[1]
+    return x.reshape(shape), y_bar.reshape(shape) if need_y else None, h_bar, scal[0], scal[1]
 
 
 class Recording:
@@ -311,9 +313,10 @@ def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_
     return x.reshape(shape), rec
 
 
-def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None):
+def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True):
     """Reverse sweep of a recorded forward (x = that forward's output, unmodified).  Returns
-    (y_bar, h_bar, lam_bar, rho_bar); h_bar is None unless the forward was recorded with need_h.
+    (y_bar, h_bar, lam_bar, rho_bar); h_bar is None unless the forward was recorded with need_h, y_bar is
+    None when need_y is False (cheaper: no running sum of vbar unless h_bar needs it).
     Consumes the recording (its workspace is released)."""
     if rec.workspace is None:
         raise RuntimeError("recording already consumed")
@@ -326,11 +329,11 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None):
     stream, s_handle = _stream_of(stream, y4.device)
     ws = rec.workspace
     ws_ptr, ws_len = ws.get(0, y4.device, stream)
-    y_bar = torch.empty_like(y4)
+    y_bar = torch.empty_like(y4) if need_y else None
     h_bar = torch.empty_like(hb) if rec.want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y4.device)
     red, keep = _make_reducer(ws, rec.group) if _sharded(rec.iso, rec.group) else (None, None)
-    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr(), h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
+    head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr() if need_y else None, h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
             scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
     tail = (int(rec.iso), rec.maxit, x4.data_ptr(), ws_ptr, ws_len, s_handle,
             ctypes.byref(red) if red is not None else None)
@@ -344,7 +347,7 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None):
         _lib.check(L.admm_tvd_backward_recorded_f32(*head, rec.lam, rec.rho, *tail))
     del keep
     rec.workspace = None    # released once the stream has consumed it (caching allocator is stream-ordered)
-    return y_bar.reshape(rec.shape), h_bar, scal[0], scal[1]
+    return y_bar.reshape(rec.shape) if need_y else None, h_bar, scal[0], scal[1]
 
 
 class _TvdFFTFn(torch.autograd.Function):
@@ -368,7 +371,8 @@ class _TvdFFTFn(torch.autograd.Function):
     def backward(ctx, x_bar):
         _y, lam_t, rho_t, h_t, x = ctx.saved_tensors
         need_h = ctx.rec.want_h
-        yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar)
+        # y_bar only when y needs it (a first-layer denoiser's input does not): the sweep then skips Vsum
+        yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar, need_y=ctx.needs_input_grad[0])
         ctx.rec = None
         hg = None
         if need_h:

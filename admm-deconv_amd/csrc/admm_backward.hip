@@ -164,11 +164,13 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) rho_acc -= dv0[q] * dx0[q] + dv1[q] * dx1[q];
-            // ---- Vsum += vbar ----
-            float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
-            float4 acc = *vs;
-            acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
-            *vs = acc;
+            // ---- Vsum += vbar (null: neither y_bar nor h_bar wanted) ----
+            if (vsum) {
+                float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
+                float4 acc = *vs;
+                acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
+                *vs = acc;
+            }
         }
         if (!first_k) {
             float sb0[4] = {0, 0, 0, 0}, sb1[4] = {0, 0, 0, 0};   // sbar_k
@@ -502,10 +504,12 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) rho_acc -= dv0[q] * dx0[q] + dv1[q] * dx1[q];
-            float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
-            float4 acc = *vs;
-            acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
-            *vs = acc;
+            if (vsum) {   // null: neither y_bar nor h_bar wanted
+                float4* vs = reinterpret_cast<float4*>(vsum + (size_t)plane * MN + off);
+                float4 acc = *vs;
+                acc.x += vc.x; acc.y += vc.y; acc.z += vc.z; acc.w += vc.w;
+                *vs = acc;
+            }
             if (!first_k) {
                 // vbar_k for ISO_ADJ_B, which forms wbar = rho D vbar itself (4 B/px here and ~5 there,
                 // against 8 + 8 for a stored two-channel wbar)

@@ -956,8 +956,10 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     if (h == nullptr) kh = kw = 0;
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    rc = check_common(y, (phases & 2) ? y_bar : x_out, maxit);
+    rc = check_common(y, x_out, maxit);
     if (rc) return rc;
+    if ((phases & 2) && (reinterpret_cast<uintptr_t>(y_bar) & 15))
+        return fail(ADMM_E_INVALID, "y_bar must be a 16-byte aligned device pointer (or NULL: not needed)");
     if ((phases & 2) && (!x_bar || (reinterpret_cast<uintptr_t>(x_bar) & 15)))
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
@@ -1005,7 +1007,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     } while (0)
     if (K == 0) {
         if (phases & 2) {
-            HIPCHK(hipMemsetAsync(y_bar, 0, planes * MN * 4, s));
+            if (y_bar) HIPCHK(hipMemsetAsync(y_bar, 0, planes * MN * 4, s));
             if (h_bar && kh > 0) HIPCHK(hipMemsetAsync(h_bar, 0, (size_t)kh * kw * 4, s));
             if (lambda_bar) HIPCHK(hipMemsetAsync(lambda_bar, 0, 4, s));
             if (rho_bar) HIPCHK(hipMemsetAsync(rho_bar, 0, 4, s));
@@ -1037,7 +1039,9 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     float2* specA = reinterpret_cast<float2*>(ws + bl.f.spec0);
     float2* specB = reinterpret_cast<float2*>(ws + bl.f.spec1);
     float* sb[2] = {reinterpret_cast<float*>(ws + bl.sbA), reinterpret_cast<float*>(ws + bl.sbB)};
-    float* vsum = reinterpret_cast<float*>(ws + bl.vsum);
+    // Vsum = sum_k vbar_k feeds y_bar and the h_bar correlation only: without either the sweep skips it
+    const bool want_v = y_bar != nullptr || (h_bar != nullptr && kh > 0);
+    float* vsum = want_v ? reinterpret_cast<float*>(ws + bl.vsum) : nullptr;
     double* rpart = reinterpret_cast<double*>(ws + bl.rpart);
     float* Qp = want_h ? reinterpret_cast<float*>(ws + bl.Qp) : nullptr;
     const size_t sstride = planes * 2 * MN;
@@ -1050,7 +1054,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     if (fused_adj) {
         namespace pk = admm::plane;
         float4* dxK = reinterpret_cast<float4*>(sb[1]);
-        float* vout = kh > 0 ? vsum : y_bar;
+        float* vout = !want_v ? nullptr : kh > 0 ? vsum : y_bar;
         rc = ln.run(ADMM_K_PREP, [&] { return pk::launch_dx_lane(xK, dxK, planes, s); });
         if (rc) return rc;
         rc = ln.run(ADMM_K_ADJ, [&] {
@@ -1059,7 +1063,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         });
         if (rc) return rc;
         red_rows = (int)planes;
-    } else {
+    } else if (want_v) {
         HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
     }
     float* wbar = iso ? reinterpret_cast<float*>(ws + bl.wbar) : nullptr;
@@ -1187,9 +1191,9 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     if (rc) return rc;
     double* hcorr = kh > 0 ? reinterpret_cast<double*>(ws + bl.hcorr) : nullptr;
     double* hA = want_h ? reinterpret_cast<double*>(ws + bl.hA) : nullptr;
-    if (kh > 0) {
+    if (kh > 0 && want_v) {
         // y_bar = H vsum  (centred circular convolution, spectrally)
-        if (gen) {
+        if (y_bar && gen) {
             namespace g = admm::gen;
             const int H = M / 2 + 1;
             const g::FPlan pM = make_fplan(M), pN = make_fplan(N);
@@ -1204,7 +1208,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_inv_kernel, ggl, dim3(256), lfw, s, specB, y_bar, twM, pM, N, T); });
             if (rc) return rc;
-        } else {
+        } else if (y_bar) {
             rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_fwd(L, T, gl, flds, s, vsum, specA, twM, N); });
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] { return launch_column(N, 2, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f); });
@@ -1238,7 +1242,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             });
             if (rc) return rc;
         }
-    } else if (!fused_adj) {   // (the fused sweep wrote Vsum straight into y_bar)
+    } else if (!fused_adj && y_bar) {   // (the fused sweep wrote Vsum straight into y_bar)
         HIPCHK(hipMemcpyAsync(y_bar, vsum, planes * MN * 4, hipMemcpyDeviceToDevice, s));
     }
     rc = ln.run(ADMM_K_FINAL, [&] {

@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
     struct LAdjIn {
         float a0, a1, e0, e1, e2, vs, b0, b1;
     };
-    float* vsp = vsum + (size_t)plane * MN;
+    float* vsp = vsum ? vsum + (size_t)plane * MN : nullptr;   // null: neither y_bar nor h_bar wanted
     batched<kU>((T + 1) * M, [&](int idx) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const int j = wrap(j0 + t, N);
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
                 r.e0 = skp[o];
                 r.e1 = skp[MN + o];
             }
-            r.vs = vsp[o];
+            r.vs = vsp ? vsp[o] : 0.0f;
         }
         r.b0 = (s1p && sb_in) ? sb_in[poff + o] : 0.0f;
         r.b1 = (s1p && sb_in && own) ? sb_in[poff + MN + o] : 0.0f;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
                 d1 = r.e1 - (s1p ? clip(r.a1, tau) : 0.0f);
             }
             racc -= dv0 * d0 + dv1 * d1;
-            vsp[o] = r.vs + vc;
+            if (vsp) vsp[o] = r.vs + vc;
         }
         if (!s1p) return;   // k = 1: no sbar_0 (block-uniform)
         const float w0 = rho * dv0;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
                 d1 = sk[poff + MN + o] - (1.0f - f) * a1;
             }
             racc -= dv0 * d0 + dv1 * d1;
-            vsum[(size_t)plane * MN + o] += vc;
+            if (vsum) vsum[(size_t)plane * MN + o] += vc;
             if (sk1) {
                 const float b0 = sb_in ? sb_in[poff + o] : 0.0f, b1 = sb_in ? sb_in[poff + MN + o] : 0.0f;
                 const float w0 = rho * dv0, w1 = rho * dv1;

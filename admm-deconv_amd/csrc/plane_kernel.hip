@@ -852,9 +852,12 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         const rsrc_t s2p = k == K ? make_rsrc(dxK + plane * 64 * kPT, kS4) : make_rsrc(tb + (size_t)(k - 1) * traj_slot, kS4);
         const rsrc_t sbl = k < K ? make_rsrc(sbp, kS4) : none;
         const rsrc_t sbs = k >= 2 ? make_rsrc(sbp, kS4) : none;
-        const rsrc_t vlr = k < K ? make_rsrc(vlp, kS2) : none;
+        // without vout (neither y_bar nor h_bar wanted) the Vsum accumulator is a zero-size resource: its
+        // loads return 0 and its stores are dropped by the buffer unit, so it costs no HBM traffic
+        const bool wv = vout != nullptr;
+        const rsrc_t vlr = (k < K && wv) ? make_rsrc(vlp, kS2) : none;
         // the last step writes Vsum in the natural layout: byte r * 1024 + 16 n + 8 h
-        const rsrc_t vsr = k >= 2 ? make_rsrc(vlp, kS2) : make_rsrc(vout + plane * 65536, 65536 * 4);
+        const rsrc_t vsr = !wv ? none : k >= 2 ? make_rsrc(vlp, kS2) : make_rsrc(vout + plane * 65536, 65536 * 4);
         const unsigned vso = k >= 2 ? (unsigned)t * 8 : (unsigned)(r * 1024 + hb * 8);
         const unsigned vss = k >= 2 ? kPT * 8 : 16;
         float racc = 0.0f, tacc = 0.0f;

@@ -86,7 +86,9 @@ int admm_tvd_forward_f32(const float* y, float* x_out, int M, int N, int P, int 
  * the reference's training uses, src/train.jl:51 with src/ops/ops.jl:84-92; BASELINE config c5).
  * Recomputes the forward (writing x to x_out) while recording one state tensor per iteration, then
  * runs the reverse sweep.  Given x_bar = dL/dx it writes
- *   y_bar (device, shape of y)   h_bar (device, kw*kh floats; NULL = not needed, cheaper)
+ *   y_bar (device, shape of y; NULL = not needed, cheaper: with h_bar also NULL the reverse sweep
+ *          keeps no running sum of vbar, 8 B/px less HBM traffic per reverse step)
+ *   h_bar (device, kw*kh floats; NULL = not needed, cheaper)
  *   lambda_bar, rho_bar (device, 1 float each; NULL = not needed)
  * Both proxes: with iso != 0 the trajectory also keeps the per-pixel batch norm of every s_k and
  * each reverse step reduces R = sum over planes of s (2 w_bar - s_bar) across the batch.

@@ -323,3 +323,63 @@ def test_backward_generic_record_replay(dev):
     torch.cuda.synchronize()
     assert torch.equal(x, x2) and torch.equal(yb, yb2) and torch.equal(hb, hb2)
     assert torch.equal(lb, lb2) and torch.equal(rb, rb2)
+
+
+NO_YBAR_CASES = [
+    # (B, P, M, N, psf, iso, need_h, options): each reverse-sweep variant once
+    (2, 3, 256, 256, None, False, False, {}),                          # fused adjoint (c5 aniso layer shape)
+    (2, 1, 256, 256, ("gauss", 9, 1.5), False, False, {"FUSED_ADJ": 0}),   # 2-pass adjoint, fused trajectory
+    (2, 1, 128, 128, ("gauss", 7, 1.2), False, True, {}),              # 2-pass with h_bar (Vsum still kept)
+    (6, 3, 64, 64, None, True, False, {}),                             # iso (c5 use_iso shape class)
+    (2, 1, 100, 75, ("gauss", 5, 1.0), False, False, {}),              # runtime-length adjoint
+    (4, 1, 96, 96, None, True, False, {}),                             # runtime-length iso adjoint
+]
+
+
+@pytest.mark.parametrize("case", NO_YBAR_CASES,
+                         ids=["fused", "2pass", "2pass-hbar", "iso", "generic", "generic-iso"])
+def test_backward_without_y_bar_is_bitwise_the_same(dev, case):
+    """y_bar = NULL (the input needs no gradient, as a first-layer denoiser's does not): the reverse sweep
+    keeps no running sum of vbar (8 B/px less traffic per step), and every other gradient is bitwise the
+    one of the full sweep; through autograd, a layer whose input does not require grad gets the same
+    parameter gradients as one whose input does."""
+    B, P, M, N, spec, iso, need_h, opts = case
+    h = psf(spec, None)
+    y = torch.from_numpy(synth.make_batch(B, M, N, h, P=P)).to(dev)
+    xb = torch.randn_like(y)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    K, lam, rho = 9, 0.01, 0.05
+    import contextlib
+    with contextlib.ExitStack() as st:
+        for k, v in opts.items():
+            st.enter_context(_lib.option(k, v))
+        full = admm_deconv.tvd_fft_backward(y, xb, lam, rho, ht, iso, K, need_h=need_h)
+        part = admm_deconv.tvd_fft_backward(y, xb, lam, rho, ht, iso, K, need_h=need_h, need_y=False)
+        x, rec = admm_deconv.tvd_fft_record(y, lam, rho, ht, iso, K, need_h=need_h)
+        rep = admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_y=False)
+    torch.cuda.synchronize()
+    assert part[1] is None and rep[0] is None
+    assert torch.equal(full[0], part[0]) and torch.equal(full[0], x)
+    for i, what in ((3, "lambda_bar"), (4, "rho_bar")):
+        assert torch.equal(full[i], part[i]), what
+        assert torch.equal(full[i], rep[i - 1]), what + " (recorded)"
+    if need_h:
+        assert torch.equal(full[2], part[2]) and torch.equal(full[2], rep[1])
+
+
+def test_layer_input_without_grad_same_param_grads(dev):
+    """autograd: ADMMDeconvF2 on an input that does not require grad asks the library for no y_bar; the
+    trainable lambda's gradient equals the one of the same layer on an input that does."""
+    from admm_deconv import layers
+    y = torch.from_numpy(synth.make_batch(2, 256, 256, None, P=3)).to(dev)
+    grads = []
+    for need_y in (True, False):
+        L = layers.ADMMDeconvF2((), 12, 0.2, layers.relu1, rng=np.random.default_rng(5), device=dev)
+        L.lam.requires_grad_(True)
+        yi = y.clone().requires_grad_(need_y)
+        out = L(yi)
+        (out * out).sum().backward()
+        grads.append(L.lam.grad.clone())
+        assert (yi.grad is not None) == need_y
+    torch.cuda.synchronize()
+    assert torch.equal(grads[0], grads[1])
