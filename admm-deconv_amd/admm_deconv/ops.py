@@ -237,12 +237,13 @@ def _scalars_for(lam, rho, device, stream):
 
 
 def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, need_y=True,
-                     workspace=None, stream=None, group=None):
+                     need_rho=True, workspace=None, stream=None, group=None):
     """Adjoint of tvd_fft through all `maxit` unrolled iterations (what Zygote computes for the
     reference, src/train.jl:51).  Returns (x, y_bar, h_bar, lam_bar, rho_bar); h_bar is None without a PSF
     or when need_h is False; y_bar is None when need_y is False (the sweep then keeps no running sum of
-    vbar unless h_bar needs it: 8 B/px less traffic per reverse step).  Recomputes the forward (x is
-    returned for convenience).
+    vbar unless h_bar needs it: 8 B/px less traffic per reverse step); rho_bar is None when need_rho is
+    False (the fused and isotropic sweeps then skip s_k, which only rho_bar reads).  Recomputes the forward
+    (x is returned for convenience).
     With `group` (isotropic prox, batch sharded over the group's ranks) h_bar / lam_bar / rho_bar are
     this shard's contributions: their sum over ranks is the gradient of the whole batch."""
     shape, y4, hb = _prep(y, h)
@@ -261,7 +262,7 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     h_bar = torch.empty_like(hb) if want_h else None
     scal = torch.zeros(2, dtype=torch.float32, device=y.device)
     head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr() if need_y else None, h_bar.data_ptr() if want_h else None, scal.data_ptr(),
-            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
+            scal.data_ptr() + 4 if need_rho else None, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
     tail = (int(bool(isotropic)), int(maxit), x.data_ptr(), ws_ptr, ws_len, s_handle)
     red, keep = _make_reducer(workspace, group) if _sharded(isotropic, group) else (None, None)
     L = _lib.load()
@@ -272,7 +273,7 @@ def tvd_fft_backward(y, x_bar, lam, rho=1.0, h=None, isotropic=False, maxit=100,
     else:
         _lib.check(L.admm_tvd_backward_f32(*head, lam_h, rho_h, *tail))
     del keep
-    return x.reshape(shape), y_bar.reshape(shape) if need_y else None, h_bar, scal[0], scal[1]
+    return x.reshape(shape), y_bar.reshape(shape) if need_y else None, h_bar, scal[0], scal[1] if need_rho else None
 
 
 class Recording:
@@ -313,10 +314,11 @@ def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_
     return x.reshape(shape), rec
 
 
-def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True):
+def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True, need_rho=True):
     """Reverse sweep of a recorded forward (x = that forward's output, unmodified).  Returns
     (y_bar, h_bar, lam_bar, rho_bar); h_bar is None unless the forward was recorded with need_h, y_bar is
-    None when need_y is False (cheaper: no running sum of vbar unless h_bar needs it).
+    None when need_y is False (cheaper: no running sum of vbar unless h_bar needs it), rho_bar is None when
+    need_rho is False (cheaper: the fused and isotropic sweeps then skip s_k, read for rho_bar only).
     Consumes the recording (its workspace is released)."""
     if rec.workspace is None:
         raise RuntimeError("recording already consumed")
@@ -334,7 +336,7 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True):
     scal = torch.zeros(2, dtype=torch.float32, device=y4.device)
     red, keep = _make_reducer(ws, rec.group) if _sharded(rec.iso, rec.group) else (None, None)
     head = (y4.data_ptr(), xb.data_ptr(), y_bar.data_ptr() if need_y else None, h_bar.data_ptr() if rec.want_h else None, scal.data_ptr(),
-            scal.data_ptr() + 4, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
+            scal.data_ptr() + 4 if need_rho else None, M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
     tail = (int(rec.iso), rec.maxit, x4.data_ptr(), ws_ptr, ws_len, s_handle,
             ctypes.byref(red) if red is not None else None)
     L = _lib.load()
@@ -347,7 +349,7 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True):
         _lib.check(L.admm_tvd_backward_recorded_f32(*head, rec.lam, rec.rho, *tail))
     del keep
     rec.workspace = None    # released once the stream has consumed it (caching allocator is stream-ordered)
-    return y_bar.reshape(rec.shape) if need_y else None, h_bar, scal[0], scal[1]
+    return y_bar.reshape(rec.shape) if need_y else None, h_bar, scal[0], scal[1] if need_rho else None
 
 
 class _TvdFFTFn(torch.autograd.Function):
@@ -372,7 +374,8 @@ class _TvdFFTFn(torch.autograd.Function):
         _y, lam_t, rho_t, h_t, x = ctx.saved_tensors
         need_h = ctx.rec.want_h
         # y_bar only when y needs it (a first-layer denoiser's input does not): the sweep then skips Vsum
-        yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar, need_y=ctx.needs_input_grad[0])
+        yb, hb, lb, rb = tvd_fft_backward_recorded(ctx.rec, x, x_bar, need_y=ctx.needs_input_grad[0],
+                                                   need_rho=ctx.needs_input_grad[2])
         ctx.rec = None
         hg = None
         if need_h:

@@ -484,15 +484,16 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                 a1[0] = b.x; a1[1] = b.y; a1[2] = b.z; a1[3] = b.w;
             }
             // ---- rho_bar: -<D vbar, D x_k> ----
-            float dx0[4], dx1[4];
-            if (last_k) {
+            // (xK / sk null: rho_bar not wanted, D x_k reads as 0 and costs no traffic)
+            float dx0[4] = {0, 0, 0, 0}, dx1[4] = {0, 0, 0, 0};
+            if (last_k && xK) {
                 const float* xp = xK + (size_t)plane * MN;
                 const float4 xc = *reinterpret_cast<const float4*>(xp + off);
                 const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
                 const float xl = xp[(size_t)(j0 + t) * M + ((i - 1) & (M - 1))];
                 dx0[0] = xc.x - xq.x; dx0[1] = xc.y - xq.y; dx0[2] = xc.z - xq.z; dx0[3] = xc.w - xq.w;
                 dx1[0] = xc.x - xl; dx1[1] = xc.y - xc.x; dx1[2] = xc.z - xc.y; dx1[3] = xc.w - xc.z;
-            } else {
+            } else if (!last_k && sk) {
                 const float4 a = *reinterpret_cast<const float4*>(sk + poff + off);
                 const float4 b = *reinterpret_cast<const float4*>(sk + poff + MN + off);
                 const float c0[4] = {a.x, a.y, a.z, a.w}, c1[4] = {b.x, b.y, b.z, b.w};

@@ -1042,6 +1042,8 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     // Vsum = sum_k vbar_k feeds y_bar and the h_bar correlation only: without either the sweep skips it
     const bool want_v = y_bar != nullptr || (h_bar != nullptr && kh > 0);
     float* vsum = want_v ? reinterpret_cast<float*>(ws + bl.vsum) : nullptr;
+    // s_k and D x_K enter rho_bar's <D vbar, D x_k> only (fused and iso sweeps skip them without rho_bar)
+    const bool want_rho = rho_bar != nullptr;
     double* rpart = reinterpret_cast<double*>(ws + bl.rpart);
     float* Qp = want_h ? reinterpret_cast<float*>(ws + bl.Qp) : nullptr;
     const size_t sstride = planes * 2 * MN;
@@ -1053,10 +1055,12 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     int red_rows = K * bl.nblk_line;   // rows of (rho_bar, tau_bar) partials
     if (fused_adj) {
         namespace pk = admm::plane;
-        float4* dxK = reinterpret_cast<float4*>(sb[1]);
+        float4* dxK = want_rho ? reinterpret_cast<float4*>(sb[1]) : nullptr;
         float* vout = !want_v ? nullptr : kh > 0 ? vsum : y_bar;
-        rc = ln.run(ADMM_K_PREP, [&] { return pk::launch_dx_lane(xK, dxK, planes, s); });
-        if (rc) return rc;
+        if (want_rho) {
+            rc = ln.run(ADMM_K_PREP, [&] { return pk::launch_dx_lane(xK, dxK, planes, s); });
+            if (rc) return rc;
+        }
         rc = ln.run(ADMM_K_ADJ, [&] {
             return pk::launch_plane_adj(x_bar, ws + bl.f.F, reinterpret_cast<const float4*>(tr.s), dxK,
                                        reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s);
@@ -1161,7 +1165,8 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         // isotropic: ISO_ADJ_A (plane groups) -> ISO_ADJ_R (batch R map, tau_bar) -> ISO_ADJ_B (per plane)
         const float* nrm1 = k >= 2 ? tr.nrm + (size_t)(k - 2) * MN : nullptr;
         rc = ln.run(ADMM_K_ADJ, [&] {
-            return launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1, skk, xK,
+            return launch_iso_adj_a(L, T, dim3(N / T, (unsigned)ngi), iso_a_lds(M, T) + 8 * 16, s, specB, sk1,
+                             want_rho ? skk : nullptr, want_rho ? xK : nullptr,
                              nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)planes, iso_group(planes), prm,
                              k == 1 ? 1 : 0, k == K ? 1 : 0);
         });

@@ -849,7 +849,8 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, none, nullptr, t, hb);
         line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
         const rsrc_t s1p = k >= 2 ? make_rsrc(tb + (size_t)(k - 2) * traj_slot, kS4) : none;
-        const rsrc_t s2p = k == K ? make_rsrc(dxK + plane * 64 * kPT, kS4) : make_rsrc(tb + (size_t)(k - 1) * traj_slot, kS4);
+        // s_k / D x_K feed only rho_bar's <D vbar, D x_k>: without dxK (rho_bar not wanted) they read as 0
+        const rsrc_t s2p = !dxK ? none : k == K ? make_rsrc(dxK + plane * 64 * kPT, kS4) : make_rsrc(tb + (size_t)(k - 1) * traj_slot, kS4);
         const rsrc_t sbl = k < K ? make_rsrc(sbp, kS4) : none;
         const rsrc_t sbs = k >= 2 ? make_rsrc(sbp, kS4) : none;
         // without vout (neither y_bar nor h_bar wanted) the Vsum accumulator is a zero-size resource: its

@@ -357,8 +357,16 @@ def test_backward_without_y_bar_is_bitwise_the_same(dev, case):
         part = admm_deconv.tvd_fft_backward(y, xb, lam, rho, ht, iso, K, need_h=need_h, need_y=False)
         x, rec = admm_deconv.tvd_fft_record(y, lam, rho, ht, iso, K, need_h=need_h)
         rep = admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_y=False)
+        # neither y_bar nor rho_bar (ADMMDeconvF2's fixed rho): s_k is not read either
+        lo = admm_deconv.tvd_fft_backward(y, xb, lam, rho, ht, iso, K, need_h=need_h, need_y=False, need_rho=False)
+        x, rec = admm_deconv.tvd_fft_record(y, lam, rho, ht, iso, K, need_h=need_h)
+        rep2 = admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_y=False, need_rho=False)
     torch.cuda.synchronize()
     assert part[1] is None and rep[0] is None
+    assert lo[1] is None and lo[4] is None and rep2[0] is None and rep2[3] is None
+    assert torch.equal(full[3], lo[3]) and torch.equal(full[3], rep2[2]), "lambda_bar without rho_bar"
+    if need_h:
+        assert torch.equal(full[2], lo[2]) and torch.equal(full[2], rep2[1])
     assert torch.equal(full[0], part[0]) and torch.equal(full[0], x)
     for i, what in ((3, "lambda_bar"), (4, "rho_bar")):
         assert torch.equal(full[i], part[i]), what
@@ -368,14 +376,16 @@ def test_backward_without_y_bar_is_bitwise_the_same(dev, case):
 
 
 def test_layer_input_without_grad_same_param_grads(dev):
-    """autograd: ADMMDeconvF2 on an input that does not require grad asks the library for no y_bar; the
-    trainable lambda's gradient equals the one of the same layer on an input that does."""
+    """autograd: ADMMDeconvF2 (fixed rho) on an input that does not require grad asks the library for
+    neither y_bar nor rho_bar; the trainable lambda's gradient equals the one of the same layer on an input
+    that does (whose rho is made trainable too, so that the full sweep runs)."""
     from admm_deconv import layers
     y = torch.from_numpy(synth.make_batch(2, 256, 256, None, P=3)).to(dev)
     grads = []
     for need_y in (True, False):
         L = layers.ADMMDeconvF2((), 12, 0.2, layers.relu1, rng=np.random.default_rng(5), device=dev)
         L.lam.requires_grad_(True)
+        L.rho.requires_grad_(need_y)
         yi = y.clone().requires_grad_(need_y)
         out = L(yi)
         (out * out).sum().backward()
