@@ -144,16 +144,16 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
             if (!own) s1[0] = s1[1] = s1[2] = s1[3] = 0.0f;
         }
         if (own) {
-            // ---- rho_bar: -<Dvb, D x_k> ----
-            float dx0[4], dx1[4];
-            if (last_k) {
+            // ---- rho_bar: -<Dvb, D x_k> (xK / sk null: rho_bar not wanted, no reads) ----
+            float dx0[4] = {0, 0, 0, 0}, dx1[4] = {0, 0, 0, 0};
+            if (last_k && xK) {
                 const float* xp = xK + (size_t)plane * MN;
                 const float4 xc = *reinterpret_cast<const float4*>(xp + off);
                 const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
                 const float xl = xp[(size_t)((j0 + t) & (N - 1)) * M + ((i - 1) & (M - 1))];
                 dx0[0] = xc.x - xq.x; dx0[1] = xc.y - xq.y; dx0[2] = xc.z - xq.z; dx0[3] = xc.w - xq.w;
                 dx1[0] = xc.x - xl; dx1[1] = xc.y - xc.x; dx1[2] = xc.z - xc.y; dx1[3] = xc.w - xc.z;
-            } else {
+            } else if (!last_k && sk) {
                 float a4[4], b4[4];
                 load_s_quad<LN>(sk + poff, (j0 + t) & (N - 1), i, M, MN, true, a4, b4);
 #pragma unroll

@@ -1156,7 +1156,8 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         double* rp = rpart + (size_t)(K - k) * bl.nblk_line * 2;
         if (!iso) {
             rc = ln.run(ADMM_K_ADJ, [&] {
-                return launch_line_adj(L, T, gl, alds, s, specB, sk1, skk, xK, sbi, sbo, vsum, specA, rp, twM, N, prm,
+                return launch_line_adj(L, T, gl, alds, s, specB, sk1, want_rho ? skk : nullptr, want_rho ? xK : nullptr,
+                                       sbi, sbo, vsum, specA, rp, twM, N, prm,
                                 k == 1 ? 1 : 0, k == K ? 1 : 0, ln_traj);
             });
             if (rc) return rc;
