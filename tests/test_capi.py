@@ -146,3 +146,14 @@ def test_replay_without_recording_is_rejected():
                                           0, 5, fake, fake, 1 << 34, None, None)
     assert rc == _lib.ADMM_E_INVALID
     assert b"no recording" in L.admm_last_error()
+
+
+def test_backward_y_bar_optional_but_aligned():
+    """y_bar may be NULL (input needs no gradient), but a given y_bar must be 16-byte aligned: rejected with
+    ADMM_E_INVALID before any device work."""
+    L = _lib.load()
+    fake = 1 << 21
+    rc = L.admm_tvd_backward_f32(fake, fake, fake + 4, None, None, None, 64, 64, 1, 1, None, 0, 0, 0.1, 1.0, 0, 5,
+                                 fake, fake, 1 << 30, None)
+    assert rc == _lib.ADMM_E_INVALID
+    assert b"y_bar" in L.admm_last_error()
