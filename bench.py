@@ -162,21 +162,21 @@ def bench_c5(args, dev):
             kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
     roof = None
     if not args.iso and kernels.get("adjoint", {}).get("launches_per_step") == len(branch):
-        # fused reverse sweep (plane256_adj_kernel, one launch per layer), per pixel: s_{k-1} (K-1 steps),
-        # s_k / D x_K (K), sbar_k in (K-1), sbar_{k-1} out (K-1) at 8 B; Vsum in (K-1) and out (K) at 4 B;
-        # x_bar in (4 B): (40 K - 24) B/px
+        # fused reverse sweep (plane256_adj_kernel, one launch per layer).  The input and rho need no gradient,
+        # so the sweep gets neither y_bar nor rho_bar and reads no Vsum and no s_k; per pixel: s_{k-1},
+        # sbar_k in, sbar_{k-1} out (K-1 steps each, 8 B) and x_bar in (4 B): (24 K - 20) B/px
         planes = B * P
-        per_launch = planes * M * N * (40 * K - 24)
+        per_launch = planes * M * N * (24 * K - 20)
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "adjoint (plane256_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("c5", "adjoint"),
                 "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": round(a["avg_ms"], 5)}
     elif not args.iso and "adjoint" in kernels:
-        # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1}, s_k,
-        # sbar_k, sbar_{k-1} (8 M N each) and Vsum read + write (4 M N each) -- the interior steps
+        # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1},
+        # sbar_k, sbar_{k-1} (8 M N each; no s_k and no Vsum: neither rho_bar nor y_bar requested)
         planes = B * P
-        per_launch = planes * (16 * (M // 2) * N + 40 * M * N)
+        per_launch = planes * (16 * (M // 2) * N + 24 * M * N)
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "adjoint (line_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
