@@ -12,6 +12,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .ops import Workspace
 
 __all__ = ["gmsd", "gmsd_loss", "ssim", "ssim_loss", "ssim_loss_fast", "ssim_kernel", "peak_snr", "mse"]
 
@@ -36,13 +37,12 @@ def _prep(x, y):
 
 
 def _workspace(dev, nbytes):
-    buf = _ws.get(dev)
-    if buf is None or buf.numel() < nbytes + 256:
-        buf = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=dev)
-        _ws[dev] = buf
-    p = buf.data_ptr()
-    off = (-p) % 256
-    return p + off, buf.numel() - off
+    """Scratch of a metrics call, one per (device, stream) as the solver's default workspaces
+    (ops.Workspace): two losses enqueued on different streams never share scratch, and a growing
+    reallocation is stream-ordered (the buffer is marked as used on the stream it serves)."""
+    stream = torch.cuda.current_stream(dev)
+    ws = _ws.setdefault((dev, stream.cuda_stream), Workspace())
+    return ws.get(nbytes, dev, stream)
 
 
 def _ws_for(x4, ks, grad):

@@ -34,7 +34,8 @@ class Workspace:
         self._buf = None
 
     def get(self, nbytes, device, stream=None):
-        if self._buf is None or self._buf.numel() < nbytes or self._buf.device != device:
+        # + 256: room for the 256-B alignment of the returned pointer
+        if self._buf is None or self._buf.numel() < nbytes + 256 or self._buf.device != device:
             self._buf = torch.empty(max(nbytes, 256) + 256, dtype=torch.uint8, device=device)
         if stream is not None and isinstance(stream, torch.cuda.Stream) and stream != torch.cuda.current_stream(device):
             self._buf.record_stream(stream)
@@ -341,7 +342,7 @@ def tvd_fft_backward_recorded(rec, x, x_bar, *, stream=None, need_y=True, need_r
             ctypes.byref(red) if red is not None else None)
     L = _lib.load()
     if rec.dv is not None:
-        if stream != torch.cuda.current_stream(y4.device):
+        if isinstance(stream, torch.cuda.Stream) and stream != torch.cuda.current_stream(y4.device):
             for t in (rec.dv.lam, rec.dv.rho):
                 t.record_stream(stream)
         _lib.check(L.admm_tvd_backward_recorded_dev_f32(*head, *rec.dv.ptrs, *tail))

@@ -7,8 +7,10 @@ communication.  The only exchange is optional: gathering every rank's outputs to
 ranks) after the solve -- `torch.distributed` with backend "nccl" is RCCL over xGMI on MI355X;
 with "gloo" the same code runs on CPU tensors for the multi-process tests.
 
-The isotropic prox couples the whole batch (pixelnorm over dims 3,4, ops.jl:6), so it does NOT
-shard this way; see DESIGN.md (it needs a per-iteration all-reduce of an M x N map).
+The isotropic prox couples the whole batch (pixelnorm over dims 3,4, ops.jl:6), so its shards need a
+per-iteration all-reduce of an M x N map.  That exchange lives inside the solve: pass `group=` to
+`tvd_fft` / the layers (ops._make_reducer hands the library an admm_batch_reducer that all-reduces the
+map over the group); this module only shards batches and gathers outputs.
 """
 from __future__ import annotations
 
@@ -61,18 +63,19 @@ class ShardGather:
     With "gloo" (CPU collectives: the multi-process tests) the same schedule runs synchronously,
     CUDA slices going through host copies.
 
-    `gathered()` returns rank dst's (world * B_local, ...) result of the last step (None elsewhere);
-    call it after the device work has completed (torch.cuda.synchronize or `wait()`).
+    `gathered()` returns rank dst's (world * B_local, ...) result of the last step (None elsewhere).  It is
+    a collective (every rank calls it): it makes the device work of every rank complete and, for "ipc",
+    runs a barrier, so the peer writes into rank dst's buffer have landed.  The receive side is double
+    buffered by step parity: the returned tensor stays valid until two more steps have been issued.
 
     engine="ipc" moves the outputs without any collective kernel: rank dst shares its receive buffer
     once through a HIP IPC handle, and every rank copies each solved slice into its part of it with an
     async device copy on the second stream.  The HIP runtime hands peer copies of >= ROC_P2P_SDMA_SIZE
     to the SDMA engines, so no CU is held while the bytes cross xGMI.  An RCCL gather keeps kernel blocks
     resident for the whole transfer, and the fused solve needs every CU: one such block costs it
-    ~0.8 ms per 1.2 ms (tools/contend.py).  With ipc the receive buffer is complete once
-    every rank has finished its copies, i.e. after `wait()`, a device synchronize and a barrier on all
-    ranks.  If any rank cannot open the handle, every rank falls back to engine "rccl" (`self.engine`
-    says which ran)."""
+    ~0.8 ms per 1.2 ms (tools/contend.py).  With ipc a receive buffer is complete once
+    every rank has finished its copies (what `gathered()` waits for).  If any rank cannot open the
+    handles, every rank falls back to engine "rccl" (`self.engine` says which ran)."""
 
     def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0, engine="rccl"):
         self.y = y_local
@@ -92,11 +95,11 @@ class ShardGather:
             self.engine = "ipc" if self._ipc_setup(y_local) else "rccl"
         self.async_comm = self.cuda and self.world > 1 and (not self.gloo or self.engine == "ipc")
         if self.engine == "ipc":
-            pass   # self.recv (rank dst) / self.remote (others) set by _ipc_setup
+            pass   # self.recv (rank dst) / self.remote (others): two buffers each, set by _ipc_setup
         elif self.world > 1 and self.rank == dst:
             full = (self.world * n,) + tuple(y_local.shape[1:])
             dev = "cpu" if self.gloo else y_local.device
-            self.recv = torch.empty(full, dtype=y_local.dtype, device=dev)
+            self.recv = [torch.empty(full, dtype=y_local.dtype, device=dev) for _ in range(2)]
         else:
             self.recv = None
         if self.async_comm:
@@ -115,8 +118,8 @@ class ShardGather:
         obj = [None]
         try:
             if self.rank == self.dst:
-                self.recv = torch.empty(full, dtype=y_local.dtype, device=y_local.device)
-                obj = [reduce_tensor(self.recv)[1]]
+                self.recv = [torch.empty(full, dtype=y_local.dtype, device=y_local.device) for _ in range(2)]
+                obj = [[reduce_tensor(r)[1] for r in self.recv]]
         except Exception:   # noqa: BLE001 -- any failure selects the RCCL path on every rank
             ok = 0
         dist.broadcast_object_list(obj, src=self.dst, group=self.group)
@@ -124,12 +127,13 @@ class ShardGather:
             if self.rank != self.dst:
                 if obj[0] is None:
                     raise RuntimeError("no handle")
-                self.remote = rebuild_cuda_tensor(*obj[0])
-                if tuple(self.remote.shape) != full:
+                self.remote = [rebuild_cuda_tensor(*h) for h in obj[0]]
+                if any(tuple(r.shape) != full for r in self.remote):
                     raise RuntimeError("shape mismatch")
                 # one real copy through the path the steps use (peer access, engine choice): any error
                 # here selects RCCL instead of failing mid-run; the slice is overwritten by the first step
-                self.remote[self.rank * n: self.rank * n + 1].copy_(y_local[:1])
+                for r in self.remote:
+                    r[self.rank * n: self.rank * n + 1].copy_(y_local[:1])
                 torch.cuda.synchronize(y_local.device)
         except Exception:   # noqa: BLE001
             ok = 0
@@ -145,16 +149,16 @@ class ShardGather:
         receive buffer (nothing reads it during the steps), so it copies nothing."""
         if self.engine == "ipc" and self.rank == self.dst:
             n = self.y.shape[0]
-            return self.recv[self.rank * n: (self.rank + 1) * n]
+            return self.recv[b][self.rank * n: (self.rank + 1) * n]
         return self.out[b]
 
-    def _parts(self, c):
-        """rank dst's receive views for chunk c of every rank (rank r's chunk lands at r * n + start)."""
+    def _parts(self, c, b):
+        """rank dst's receive views (buffer b) for chunk c of every rank (rank r's chunk lands at r * n + start)."""
         if self.recv is None:
             return None
         n = self.y.shape[0]
         s, k = self.bounds[c]
-        return [self.recv[r * n + s: r * n + s + k] for r in range(self.world)]
+        return [self.recv[b][r * n + s: r * n + s + k] for r in range(self.world)]
 
     def step(self):
         b = self.i & 1
@@ -172,12 +176,12 @@ class ShardGather:
                     self.comm.wait_event(done)
                     if self.engine == "ipc":
                         n = self.y.shape[0]
-                        self.remote[self.rank * n + s: self.rank * n + s + k].copy_(out[s:s + k], non_blocking=True)
+                        self.remote[b][self.rank * n + s: self.rank * n + s + k].copy_(out[s:s + k], non_blocking=True)
                     else:
-                        dist.gather(out[s:s + k], self._parts(c), dst=self.dst, group=self.group)
+                        dist.gather(out[s:s + k], self._parts(c, b), dst=self.dst, group=self.group)
             else:
                 src = out[s:s + k].cpu() if (self.gloo and self.cuda) else out[s:s + k]
-                dist.gather(src, self._parts(c), dst=self.dst, group=self.group)
+                dist.gather(src, self._parts(c, b), dst=self.dst, group=self.group)
         if self.async_comm:
             ev = torch.cuda.Event()
             ev.record(self.comm)
@@ -194,6 +198,12 @@ class ShardGather:
         return self._out((self.i - 1) & 1)
 
     def gathered(self):
+        """Rank dst's gathered batch of the last step (None on other ranks).  Collective: call on every rank."""
         if self.world == 1:
             return self.local()
-        return self.recv
+        self.wait()
+        if self.cuda:
+            torch.cuda.synchronize(self.y.device)
+        if self.engine == "ipc":
+            dist.barrier(group=self.group)   # every peer's copies into rank dst's buffer have completed
+        return None if self.recv is None else self.recv[(self.i - 1) & 1]

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
                                                             double* __restrict__ part, const float2* __restrict__ twM,
                                                             int N, const float* __restrict__ prm, int first_k /*k==1*/,
                                                             int last_k /*k==K*/) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -372,7 +372,7 @@ __global__ void reduce_planes_kernel(const float* __restrict__ Qp, double* __res
 __global__ void grads_final_kernel(const double* __restrict__ rt, const double* __restrict__ hb_corr,
                                    const double* __restrict__ hb_A, int ntaps, const float* __restrict__ prm,
                                    float* __restrict__ lam_bar, float* __restrict__ rho_bar, float* __restrict__ h_bar) {
-    const float lam = prm[2]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float lam = prm[2]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) {
         const double tau_bar = rt[1];
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                                                              double* __restrict__ part, const float2* __restrict__ twM,
                                                              int N, int planes, int G, const float* __restrict__ prm,
                                                              int first_k, int last_k) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     // nrm1 = Nrm_{k-1} (k >= 2), nrm0 = Nrm_{k-2} (k >= 3; for D x_k = s_k - psi(s_{k-1}) we need f_{k-1}
     // only: nrm0 is unused but kept for symmetry of the call -- psi(s_{k-1}) uses nrm1)
     (void)nrm0;
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
 __global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __restrict__ rpartial, float* __restrict__ Rmap,
                                                              const float* __restrict__ nrm1, int ngroups, size_t MN,
                                                              const float* __restrict__ prm, double* __restrict__ part) {
-    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0];   // device-resident scalars (setup_kernel)
     __shared__ double red[2 * (kThreads / 64)];
     __shared__ float gred[kThreads];
     float tacc = 0.0f;
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
                                                              const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                              float2* __restrict__ spec0, const float2* __restrict__ twM,
                                                              int N, const float* __restrict__ prm) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;

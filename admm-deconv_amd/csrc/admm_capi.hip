@@ -28,6 +28,7 @@
 #include "admm_generic_bwd.hip"
 #include "plane_api.hpp"
 #include "smooth_api.hpp"
+#include "layout.hpp"
 
 namespace {
 
@@ -55,16 +56,7 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
-
-struct Layout {
-    size_t prm, twM, twN, C, G, hty, sA, sB, spec0, spec1, fmap, part, F, xg, total;
-};
-
-// The tuned kernels cover power-of-two 4 <= M <= 1024, 2 <= N <= 1024; every other shape from 2 x 2 up
-// to 4096 x 4096 runs the runtime-length path (admm_generic.hip).
-bool pow2_shape(int M, int N) { return is_pow2(M) && is_pow2(N) && M >= 4 && M <= 1024 && N >= 2 && N <= 1024; }
-bool generic_shape(int M, int N) { return !pow2_shape(M, N); }
+using namespace admm::layout;
 constexpr int kGenMax = 4096;
 
 // Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
@@ -73,54 +65,10 @@ constexpr int kGenMax = 4096;
 std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
 int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 
-// The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox;
 // ADMM_OPT_FUSED = 0 forces the 2-pass path (tests compare the two).
-bool fused_shape(int M, int N, bool iso) { return M == 256 && N == 256 && !iso; }
 bool fused_enabled() { return opt(ADMM_OPT_FUSED) != 0; }
 // ADMM_OPT_FUSED_ADJ = 0 keeps the 2-pass reverse sweep (line_adj + column) on a fused trajectory
 bool fused_adj_enabled() { return opt(ADMM_OPT_FUSED_ADJ) != 0; }
-size_t fused_tables_bytes() { return admm::plane::tables_bytes(); }
-
-size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
-
-// Planes per isotropic plane-group block (ISO_A / ISO_ADJ_A keep a group's partial batch sums in
-// registers; ISO_R / ISO_ADJ_R add the groups' maps).  At most 64 groups: enough blocks to fill the chip
-// (64 x N/T), while the group maps stay small (64 x M x N floats).  16 planes per group for every batch
-// left the c5 batch (192 planes) at 12 x 32 = 384 blocks, a block and a half per CU.
-int iso_group(size_t planes) { return (int)((planes + 63) / 64); }
-int iso_ngroups(size_t planes) {
-    const int g = iso_group(planes);
-    return (int)((planes + g - 1) / g);
-}
-
-Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
-    Layout L{};
-    size_t off = 0;
-    auto take = [&](size_t bytes) {
-        size_t o = off;
-        off = align_up(off + bytes);
-        return o;
-    };
-    const size_t MN = (size_t)M * N;
-    L.prm = take(16);   // {tau, rho, lambda} resolved on the device (setup_kernel / scal_kernel)
-    L.twM = take((size_t)M * 8);
-    L.twN = take((size_t)N * 8);
-    L.C = take((size_t)(M / 2 + 1) * N * 4);
-    L.G = psf ? take((size_t)(M / 2 + 1) * N * 8) : 0;
-    L.hty = psf ? take(planes * MN * 4) : 0;
-    L.sA = take(planes * 2 * MN * 4);
-    L.sB = take(planes * 2 * MN * 4);
-    // N lines x M/2 complex (packed) -- or M/2 + 1 bins per line on the generic path
-    const size_t spec_bytes = generic_shape(M, N) ? planes * (size_t)(M / 2 + 1) * N * 8 : planes * MN * 4;
-    L.spec0 = take(spec_bytes);
-    L.spec1 = take(spec_bytes);
-    L.xg = generic_shape(M, N) ? take(planes * MN * 4) : 0;
-    L.fmap = iso ? take(MN * 4) : 0;
-    L.part = iso ? take((size_t)iso_ngroups(planes) * MN * 4) : 0;
-    L.F = fused_shape(M, N, iso) ? take(fused_tables_bytes()) : 0;
-    L.total = off;
-    return L;
-}
 
 // ---- tile-size policy ------------------------------------------------------------------------
 // T = lines per line-kernel block (power of two dividing N); KB = slots per column-kernel block.
@@ -372,6 +320,9 @@ int check_shape(int M, int N, int P, int B, int kh, int kw, int iso) {
 // waves of the fused kernel (one workgroup per CU).
 constexpr size_t kChunkPlanes = 255 * 256;
 size_t launch_planes(size_t planes) { return planes < kChunkPlanes ? planes : kChunkPlanes; }
+// The isotropic prox couples the whole batch through the per-pixel norm (ops.jl:6), so an isotropic
+// batch is never split: it runs as one launch sequence of up to 65535 planes (check_shape's limit).
+size_t chunk_planes(size_t planes, bool iso) { return iso ? planes : launch_planes(planes); }
 
 }  // namespace
 
@@ -385,7 +336,7 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    *out_bytes = make_layout(M, N, launch_planes((size_t)P * B), kh > 0, iso != 0).total;
+    *out_bytes = make_layout(M, N, chunk_planes((size_t)P * B, iso != 0), kh > 0, iso != 0).total;
     return ADMM_OK;
 }
 
@@ -766,8 +717,11 @@ constexpr int kRedParts = 256;          // first-stage blocks per column of a lo
 
 BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h, bool iso) {
     BwdLayout b{};
-    b.f = make_layout(M, N, planes, kh > 0, iso);
-    size_t off = b.f.total;
+    const BwdHead hd = bwd_head(M, N, planes, kh, maxit, want_h, iso);
+    b.f = hd.f;
+    b.traj_s = hd.traj_s, b.traj_v = hd.traj_v, b.sig = hd.sig, b.sbA = hd.sbA, b.sbB = hd.sbB, b.vsum = hd.vsum;
+    b.traj_n = hd.traj_n;
+    size_t off = hd.end;
     auto take = [&](size_t bytes) {
         size_t o = off;
         off = align_up(off + bytes);
@@ -778,16 +732,8 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
     const bool gen = generic_shape(M, N);
     const int T = gen ? gen_T(M, N) : bwd_line_T(M, N, iso);
     const bool hq = want_h && kh > 0;
-    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * 2 * MN * 4);
-    // forward dim-2 spectra per iteration: packed M/2 x N (power of two) or M/2+1 x N bins (generic)
-    b.traj_v = hq ? take((size_t)K * planes * (gen ? (size_t)(M / 2 + 1) * N * 8 : MN * 4)) : 0;
-    b.sig = hq ? take((size_t)(M / 2 + 1) * N * 16) : 0;
-    b.sbA = take(planes * 2 * MN * 4);
-    b.sbB = take(planes * 2 * MN * 4);
-    b.vsum = take(planes * MN * 4);
     if (iso) {
         const size_t ng = iso_ngroups(planes);
-        b.traj_n = take((size_t)(K > 1 ? K - 1 : 1) * MN * 4);
         b.wbar = take(planes * MN * 4);   // vbar_k handed from ISO_ADJ_A to ISO_ADJ_B
         b.Rmap = take(MN * 4);
         b.Rpart = take(ng * MN * 4);
@@ -899,15 +845,21 @@ int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const floa
 struct RecTag {
     int M, N, P, B, kh, kw, iso, maxit, want_h;
     int opts[ADMM_OPT_COUNT];
+    // host-value lambda / rho of the recording (0, 0 for device-resident scalars, which the host cannot
+    // read without a synchronisation): a replay with other host values is refused
+    float lam, rho;
+    int dev_scalars;
     bool operator==(const RecTag& o) const { return std::memcmp(this, &o, sizeof(RecTag)) == 0; }
 };
 std::mutex g_rec_mu;
 std::unordered_map<const void*, RecTag> g_rec;
 
-RecTag make_tag(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, bool want_h) {
+RecTag make_tag(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, bool want_h, const admm::ScalarSrc& sc) {
     RecTag t;
     std::memset(&t, 0, sizeof(t));
     t.M = M, t.N = N, t.P = P, t.B = B, t.kh = kh, t.kw = kw, t.iso = iso != 0, t.maxit = maxit, t.want_h = want_h;
+    t.dev_scalars = sc.lam != nullptr;
+    if (!t.dev_scalars) t.lam = sc.lam_v, t.rho = sc.rho_v;
     for (int i = 0; i < ADMM_OPT_COUNT; ++i) t.opts[i] = opt(i);
     return t;
 }
@@ -931,7 +883,7 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rc = check_common(y, x_out, maxit);
     if (rc) return rc;
     const size_t planes = (size_t)P * B;
-    const size_t chunk = launch_planes(planes);   // check_shape kept iso batches to one chunk
+    const size_t chunk = chunk_planes(planes, iso != 0);   // an isotropic batch is one chunk
     const Layout lay = make_layout(M, N, chunk, kh > 0, iso != 0);
     rc = check_ws(workspace, workspace_bytes, lay.total);
     if (rc) return rc;
@@ -970,7 +922,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
-    const RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h);
+    const RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h, sc);
     if (phases == 2) {
         std::lock_guard<std::mutex> lk(g_rec_mu);
         auto it = g_rec.find(workspace);
@@ -978,8 +930,8 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             return fail(ADMM_E_INVALID, "workspace holds no recording (admm_tvd_forward_record_* first; a plain forward "
                                         "on the same workspace overwrites it)");
         if (!(it->second == tag))
-            return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request or "
-                                        "library options changed between record and replay)");
+            return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request, "
+                                        "lambda / rho or library options changed between record and replay)");
         g_rec.erase(it);
     } else {
         std::lock_guard<std::mutex> lk(g_rec_mu);
@@ -1026,11 +978,9 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         if (rc) return rc;
     }
     if (!(phases & 2)) return ln.finish();
-    if (!(phases & 1)) {
-        // replay: resolve lambda / rho again from the caller's sources (the forward's values)
-        rc = ln.run(ADMM_K_SETUP, [&] { hipLaunchKernelGGL(admm::scal_kernel, dim3(1), dim3(64), 0, s, sc, prm); });
-        if (rc) return rc;
-    }
+    // replay (phase 2 alone): the recording's {tau, rho, lambda} block is still in the workspace and is
+    // used as is -- the reverse sweep must differentiate the trajectory that was recorded, even if a
+    // device-resident lambda / rho has changed since (host values were checked against the tag above)
     // ---- reverse sweep ----
     float2* twM = reinterpret_cast<float2*>(ws + bl.f.twM);
     float2* twN = reinterpret_cast<float2*>(ws + bl.f.twN);

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
                                                        float* __restrict__ s_new, const float* __restrict__ hty,
                                                        float2* __restrict__ spec, const float2* __restrict__ twM,
                                                        FPlan pM, int N, int Tg, const float* __restrict__ prm, int first) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
                                                     const float* __restrict__ hty, float2* __restrict__ spec,
                                                     const float2* __restrict__ twM, FPlan pM, int N, int Tg,
                                                     const float* __restrict__ prm) {
-    const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void line_adj_kernel(const float* __restrict__
                                                        float* __restrict__ vsum, float2* __restrict__ spec,
                                                        double* __restrict__ part, const float2* __restrict__ twM,
                                                        FPlan pM, int N, int Tg, const float* __restrict__ prm) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void iso_adj_a_kernel(const float* __restrict_
                                                         float* __restrict__ vbar_out, float* __restrict__ vsum,
                                                         float* __restrict__ rpartial, double* __restrict__ part,
                                                         int M, int N, int planes, int G, int Tg, const float* __restrict__ prm) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float* acc = reinterpret_cast<float*>(smem_raw);
     const size_t MN = (size_t)M * N;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void iso_adj_b_kernel(const float* __restrict_
                                                         const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                         float2* __restrict__ spec, const float2* __restrict__ twM,
                                                         FPlan pM, int N, int Tg, const float* __restrict__ prm) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int M = pM.n, H = M / 2 + 1;
     const size_t MN = (size_t)M * N;

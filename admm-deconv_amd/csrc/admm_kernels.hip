@@ -60,9 +60,9 @@ __device__ __forceinline__ XBlk xcd_block() {
 // ----------------------------------------------------------------------------------------------
 // Where the solve's lambda and rho come from: device pointers (the reference's 1-element CuArrays,
 // `tvd_fft(y, λ::CGPUArray, ρ::CGPUArray, ...)`, ops.jl:99,181 -- read on the device, no host sync)
-// or, when a pointer is NULL, the host value.  setup_kernel / scal_kernel resolve them once into the
+// or, when a pointer is NULL, the host value.  setup_kernel resolves them once into the
 // workspace's scalar block prm = {tau = lambda / rho (fp32, ops.jl:20), rho, lambda}; every later
-// kernel of the solve reads prm.
+// kernel of the solve reads prm, and a recording's replay reuses the block the recording resolved.
 struct ScalarSrc {
     const float* lam;
     const float* rho;
@@ -77,10 +77,6 @@ __device__ __forceinline__ void write_prm(const ScalarSrc& sc, float* prm) {
     prm[1] = rho;
     prm[2] = lam;
 }
-__global__ void scal_kernel(ScalarSrc sc, float* __restrict__ prm) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) write_prm(sc, prm);
-}
-
 __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ twM, float2* __restrict__ twN,
                                                          float* __restrict__ Ct, float2* __restrict__ Gt,
                                                          const float* __restrict__ h, int kh, int kw, int M,
@@ -467,7 +463,7 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
                                                         const float* __restrict__ hty,
                                                         const float2* __restrict__ twM, int N, const float* __restrict__ prm,
                                                         int s_zero) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -781,7 +777,7 @@ __device__ __forceinline__ float group_sum(const float* __restrict__ part, int n
 
 __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
                                                          int ngroups, size_t MN, const float* __restrict__ prm, float* __restrict__ nrm_out) {
-    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0];   // device-resident scalars (setup_kernel)
     __shared__ float red[kThreads];
     for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
         const size_t q = base + (threadIdx.x & 63);
@@ -808,7 +804,7 @@ __global__ __launch_bounds__(kThreads) void iso_sum_kernel(const float* __restri
 
 __global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ fmap, size_t MN, const float* __restrict__ prm,
                                                            float* __restrict__ nrm_out) {
-    const float tau = prm[0];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0];   // device-resident scalars (setup_kernel)
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < MN; q += (size_t)gridDim.x * blockDim.x) {
         const float nrm = sqrtf(fmap[q]);   // fmap holds the all-reduced sum of squares
         fmap[q] = max0_nan(1.0f - tau / nrm);
@@ -820,7 +816,7 @@ template <int L, int T>
 __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict__ s_new, const float* __restrict__ fmap,
                                                          const float* __restrict__ hty, float2* __restrict__ spec0,
                                                          const float2* __restrict__ twM, int N, const float* __restrict__ prm) {
-    const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float rho = prm[1];   // device-resident scalars (setup_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;

@@ -2,6 +2,7 @@
 // tests/test_gpu_devtest.py, never by the product path).
 #include <hip/hip_runtime.h>
 
+#include "layout.hpp"
 #include "line_pair.hpp"
 #include "line_quad.hpp"
 #include "plane_kernel.hip"
@@ -118,6 +119,17 @@ int plane_debug(const float* y, float* x, const float* Cf, const float* C0b, flo
 }
 
 extern "C" {
+// Where a recording keeps its trajectory (tests read the GPU forward's own s_k / |s_k| back, to hold the
+// gradient oracle's prox masks at the GPU's, tests/test_gpu_adjoint_masked.py): byte offsets from the
+// 256-B aligned workspace base of s_1..s_{K-1} and (isotropic) of the batch norms |s_k|.
+int devtest_recording_offsets(int M, int N, int P, int B, int kh, int maxit, int want_h, int iso, size_t* traj_s,
+                              size_t* traj_n) {
+    const admm::layout::BwdHead b =
+        admm::layout::bwd_head(M, N, (size_t)P * B, kh, maxit, want_h != 0, iso != 0);
+    *traj_s = b.traj_s;
+    *traj_n = b.traj_n;
+    return 0;
+}
 // fused plane kernel (no PSF) with per-phase dumps of plane 0: dbg holds (4K) x 64 x 512 float2.
 // Cf/C0b must be the lane-native tables; hln/sln workspaces as in admm_capi.hip.
 int devtest_plane_debug(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln, float tau,

@@ -18,8 +18,9 @@ round 1 -- all pass with only these sites padded (2 to 252 s_nop 0), and fail wi
 The pass: compile the translation unit with hipcc's own pipeline (hipcc -### -save-temps) and, in the
 device assembly, put at least 2 wait states between any VMEM store with more than 64 bits of data
 (buffer/global/scratch/flat, dwordx3/x4 or b96/b128, any soffset) and a later VALU instruction that
-writes one of its data VGPRs (an `s_nop` before that VALU).  Then assemble, link and bundle exactly as
-hipcc would.
+writes one of its data VGPRs (an `s_nop` before that VALU).  The window is tracked along the
+straight-line fallthrough; a branch inside the window is padded to the full wait count first, so no
+jump target can start inside it.  Then assemble, link and bundle exactly as hipcc would.
 """
 from __future__ import annotations
 
@@ -31,6 +32,9 @@ import subprocess
 INSN = re.compile(r"^\s+([a-z][a-z0-9_]*)(\s+(.*))?$")
 VREG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
 WIDE_STORE = re.compile(r"^(buffer|global|scratch|flat)_store_(dwordx3|dwordx4|b96|b128)$")
+# control transfers: the window cannot follow the jump into its target block, so it is closed (padded)
+# before the branch instead -- every path into a block then arrives with the wait states already spent
+BRANCH = re.compile(r"^s_(branch|cbranch_\w+|setpc_b64|swappc_b64|callpc_b64|call_b64)$")
 NEED = int(os.environ.get("ADMM_HAZARD_NEED", "2"))   # wait states after the store (experiments: env)
 
 
@@ -52,6 +56,28 @@ def _store_data(mn, ops):
     return _vregs(parts[1]) if len(parts) > 1 else set()
 
 
+def _valu_dst(mn, ops):
+    """VGPRs a VALU instruction writes: operand 0, and operand 1 as well for the swap forms
+    (v_swap_b32, gfx950's v_permlane16_swap_b32 / v_permlane32_swap_b32 exchange both operands)."""
+    parts = ops.split(",")
+    dst = _vregs(parts[0])
+    if "swap" in mn and len(parts) > 1:
+        dst |= _vregs(parts[1])
+    return dst
+
+
+def _short(recent, dst=None):
+    """Wait states still missing after a wide store whose data VGPRs meet `dst` (None: any wide store)."""
+    ws, short = 0, 0
+    for data, w in reversed(recent):
+        if ws >= NEED:
+            break
+        if data and (dst is None or data & dst):
+            short = max(short, NEED - ws)
+        ws += w
+    return short
+
+
 def pad_asm(text):
     """Returns (padded assembly, number of s_nop inserted)."""
     out = []
@@ -67,19 +93,15 @@ def pad_asm(text):
             out.append(line)
             continue
         mn, ops = m.group(1), m.group(3) or ""
+        short = 0
         if mn.startswith("v_"):
-            dst = _vregs(ops.split(",")[0])
-            ws, short = 0, 0
-            for data, w in reversed(recent):
-                if ws >= NEED:
-                    break
-                if data & dst:
-                    short = max(short, NEED - ws)
-                ws += w
-            if short:
-                out.append(f"\ts_nop {short - 1}")
-                recent.append((set(), short))
-                inserted += 1
+            short = _short(recent, _valu_dst(mn, ops))
+        elif BRANCH.match(mn):
+            short = _short(recent)
+        if short:
+            out.append(f"\ts_nop {short - 1}")
+            recent.append((set(), short))
+            inserted += 1
         w = 1
         if mn == "s_nop":
             try:

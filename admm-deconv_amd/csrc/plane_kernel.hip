@@ -546,7 +546,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
                                                        float2* __restrict__ hln, float4* __restrict__ sln, const float* __restrict__ prm, int K, float2* dbg = nullptr, int stagger_ticks = 0,
                                                        float4* __restrict__ traj = nullptr, size_t traj_slot = 0) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
     // late, so that the memory-heavy row phases of two groups of CUs interleave.
     if (stagger_ticks > 0 && (blockIdx.x & 1)) {
@@ -812,7 +812,7 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
                                                            const float4* __restrict__ dxK, float4* __restrict__ sbar,
                                                            float2* __restrict__ vsl, float* __restrict__ vout,
                                                            double* __restrict__ part, const float* __restrict__ prm, int K) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel / scal_kernel)
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* colbuf = reinterpret_cast<float2*>(smem_raw);
     float2* tw = colbuf + kColF2;

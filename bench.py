@@ -376,9 +376,9 @@ def main():
             "algorithmic_bytes": alg_bytes,
             "achieved_GBps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 1),
             "frac": round(alg_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            # SURVEY.md s8d's 2-pass figure (spectrum round-trips through HBM twice per iteration)
-            "canonical_2pass_bytes": canonical_bytes(M, N, K) * planes,
-            "canonical_2pass_GBps": round(canonical_bytes(M, N, K) * planes / (ms_per_step * 1e-3) / 1e9, 1),
+            # SURVEY.md s8d's byte model of the 2-pass form (the spectrum round-trips through HBM twice per
+            # iteration): what a 2-pass solve would have to move, NOT bytes this run moved
+            "survey_2pass_model_bytes": canonical_bytes(M, N, K) * planes,
         },
     }
 

@@ -42,8 +42,18 @@ def _make_C(M, N, rho, h):
     return 1.0 / (s2 + rho * lap)
 
 
-def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100):
-    """y: (B,P,N,M) float64 tensor; lam, rho: 0-d tensors; h: (kw,kh) tensor or None.  Returns x."""
+def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, record=None):
+    """y: (B,P,N,M) float64 tensor; lam, rho: 0-d tensors; h: (kw,kh) tensor or None.  Returns x.
+
+    masks (optional): the prox's branch decisions held fixed, one entry per iteration k = 1..maxit-1 --
+    anisotropic: (m, sgn) of shape (B,P,2,N,M), m = 1[|s_k| > tau] and sgn = sign(s_k); isotropic: m of
+    shape (N,M), m = 1[||s_k|| > tau].  The prox then becomes the branch the masks select,
+        ST: z = m (s - sgn tau)            BT: z = m (1 - tau/||s||) s,
+    which equals the exact prox wherever the masks agree with s_k, and is differentiable there in the
+    same way (Zygote / autograd differentiate the selected branch).  Used to condition the gradient
+    oracle on the ST / BT masks of an fp32 implementation's own forward (tests/test_gpu_adjoint_masked.py):
+    fp32 and fp64 forwards flip different mask bits where |s_k| is within rounding of tau.
+    record (optional list): receives (s_k as (B,P,2,N,M), ||s_k|| as (N,M)) for k = 1..maxit-1."""
     B, P, N, M = y.shape
     tau = lam / rho                                                   # ops.jl:20
     C = _make_C(M, N, rho, h)
@@ -51,17 +61,29 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100):
     x = torch.zeros_like(y)
     z1 = torch.zeros_like(y); z2 = torch.zeros_like(y)
     u1 = torch.zeros_like(y); u2 = torch.zeros_like(y)
-    for _ in range(maxit):
+    for it in range(maxit):
         w1, w2 = z1 - u1, z2 - u2
         dtw = (w1 - torch.roll(w1, -1, dims=-2)) + (w2 - torch.roll(w2, -1, dims=-1))
         x = torch.fft.irfft2(C * torch.fft.rfft2(hty + rho * dtw), s=(N, M))
         d1 = x - torch.roll(x, 1, dims=-2)                             # x[i,j]-x[i,j-1]
         d2 = x - torch.roll(x, 1, dims=-1)                             # x[i,j]-x[i-1,j]
         s1, s2 = d1 + u1, d2 + u2
+        if record is not None and it < maxit - 1:
+            record.append((torch.stack([s1, s2], dim=2).detach(),
+                           torch.sqrt((s1 * s1 + s2 * s2).sum(dim=(0, 1))).detach()))
+        fixed = masks is not None and it < len(masks)
         if isotropic:
             nrm = torch.sqrt((s1 * s1 + s2 * s2).sum(dim=(0, 1), keepdim=True))
-            f = torch.clamp(1 - tau / nrm, min=0.0)
+            if fixed:
+                m = torch.as_tensor(masks[it], dtype=y.dtype)
+                f = m * (1 - tau / torch.where(m > 0, nrm, torch.ones_like(nrm)))
+            else:
+                f = torch.clamp(1 - tau / nrm, min=0.0)
             z1, z2 = f * s1, f * s2
+        elif fixed:
+            m, sg = (torch.as_tensor(a, dtype=y.dtype) for a in masks[it])
+            z1 = m[:, :, 0] * (s1 - sg[:, :, 0] * tau)
+            z2 = m[:, :, 1] * (s2 - sg[:, :, 1] * tau)
         else:
             z1 = torch.sign(s1) * torch.clamp(torch.abs(s1) - tau, min=0.0)
             z2 = torch.sign(s2) * torch.clamp(torch.abs(s2) - tau, min=0.0)
@@ -69,17 +91,28 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100):
     return x
 
 
-def tvd_fft_grads(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64):
+def tvd_fft_grads(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64, masks=None):
     """Autograd gradients of <xbar, x(y, lam, rho, h)> in `dtype` (fp64: the gradient oracle; fp32: what an
     fp32 implementation of the reference's own Zygote pass gets, used to size the gradient tolerances):
-    returns (x, ybar, hbar, lambar, rhobar)."""
+    returns (x, ybar, hbar, lambar, rhobar).  masks: see tvd_fft_torch (prox branches held fixed)."""
     y = torch.as_tensor(y, dtype=dtype).clone().requires_grad_(True)
     lam_t = torch.tensor(float(lam), dtype=dtype, requires_grad=True)
     rho_t = torch.tensor(float(rho), dtype=dtype, requires_grad=True)
     h_t = None
     if h is not None and h.size:
         h_t = torch.as_tensor(h, dtype=dtype).clone().requires_grad_(True)
-    x = tvd_fft_torch(y, lam_t, rho_t, h_t, iso, maxit)
+    x = tvd_fft_torch(y, lam_t, rho_t, h_t, iso, maxit, masks)
     (x * torch.as_tensor(xbar, dtype=dtype)).sum().backward()
     return (x.detach().numpy(), y.grad.numpy(), None if h_t is None else h_t.grad.numpy(),
             float(lam_t.grad) if lam_t.grad is not None else 0.0, float(rho_t.grad) if rho_t.grad is not None else 0.0)
+
+
+def masks_from_trajectory(s_traj, lam, rho, iso, nrm_traj=None):
+    """Prox branch masks of a recorded fp32 forward (tvd_fft_torch's `masks`): s_traj (K-1, B, P, 2, N, M)
+    = s_1..s_{K-1} as the GPU stored them; iso: nrm_traj (K-1, N, M) = the recorded batch norms.  tau is
+    formed as the library forms it, lambda / rho in fp32 (ops.jl:20)."""
+    import numpy as np
+    tau = np.float32(np.float32(lam) / np.float32(rho))
+    if iso:
+        return [(np.asarray(n) > tau).astype(np.float64) for n in nrm_traj]
+    return [((np.abs(s) > tau).astype(np.float64), np.sign(s).astype(np.float64)) for s in s_traj]

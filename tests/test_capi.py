@@ -53,6 +53,15 @@ def test_workspace_sized_for_one_chunk_of_planes():
     assert "65535" in L.admm_last_error().decode()
 
 
+def test_isotropic_batch_is_never_chunked():
+    """The isotropic prox couples the whole batch (ops.jl:6): a batch above one anisotropic chunk (65,280
+    planes) but within the isotropic limit (65,535) is sized -- and solved -- as ONE launch sequence."""
+    chunk = 255 * 256
+    iso = [_lib.workspace_bytes(4, 4, 1, n, 0, 0, True) for n in (chunk, 65300, 65535)]
+    assert iso[0] < iso[1] < iso[2]
+    assert _lib.workspace_bytes(4, 4, 1, 65300, 0, 0, False) == _lib.workspace_bytes(4, 4, 1, chunk, 0, 0, False)
+
+
 @pytest.mark.parametrize("args,code", [
     ((8192, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # M too large
     ((64, 8192, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large

@@ -1,0 +1,173 @@
+"""GPU adjoint against the gradient oracle CONDITIONED ON THE GPU FORWARD'S OWN PROX MASKS.
+
+Why: the adjoint of the unrolled ADMM loop (what Zygote computes for the reference, src/train.jl:51
+through /root/reference/src/ops/ops.jl:84-92) depends on the forward only through the ST masks
+1[|s_k| > tau] and signs (BT: 1[||s_k|| > tau]) and, for rho_bar, the values D x_k.  An fp32 forward and
+the fp64 oracle's forward flip different mask bits where |s_k| is within rounding of tau, and each flip
+moves the gradients by far more than fp32 rounding (test_gpu_backward.py bounds that against fp32
+autograd).  Here the recording's own trajectory is read back (libadmm_devtest.so gives the offsets; test
+only, the product never reads it this way), the masks are formed from it exactly as the kernels form
+them (fp32 tau = lambda / rho), and the fp64 oracle runs with its prox held at those branches
+(oracle_torch.tvd_fft_torch(masks=...)).  With the masks shared, only arithmetic separates the two:
+  y_bar, h_bar: relative L2 <= 1e-5 (whole array, no trimming); lambda_bar, rho_bar: relative <= 1e-5;
+  x: relative L2 <= 1e-5 per plane.
+Every reverse-sweep variant: 2-pass (power-of-two), fused trajectory + 2-pass sweep, fused sweep, the
+runtime-length sweep, isotropic; incl. the c4 plane at K = 50, the c5 layer shape (256^2 x 3, K = 50) and
+the case profiles/r02_grad_bounds.txt:5 flagged (128^2, 10x10 random PSF, K = 5)."""
+import contextlib
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import admm_deconv
+import oracle_torch
+from admm_deconv import _lib, synth
+from conftest import PKG_DIR, REPO
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+CASES = [
+    # (id, B, P, N, M, psf, lam, rho, K, iso, need_h, options)
+    ("2pass-32-gauss5-K6", 2, 1, 32, 32, ("gauss", 5, 1.0), 0.02, 0.1, 6, False, True, {}),
+    ("2pass-64-rand7x4-K10", 1, 2, 64, 64, ("rand", 7, 4), 0.0041, 0.021, 10, False, True, {}),
+    ("2pass-64-nopsf-K12", 2, 1, 64, 64, None, 0.05, 0.02, 12, False, True, {}),
+    ("2pass-128-rand10-K5", 1, 1, 128, 128, ("rand", 10, 10), 0.01, 0.05, 5, False, True, {}),
+    ("2pass-16x32-K1", 1, 1, 16, 32, ("gauss", 3, 0.8), 0.02, 0.1, 1, False, True, {}),
+    ("2pass-256-c2-K25-hbar", 2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, False, True, {}),
+    ("2pass-512-c4plane-K50", 1, 1, 512, 512, ("gauss", 15, 2.5), 0.0041, 0.021, 50, False, True, {}),
+    ("fusedtraj-2pass-256-K12", 2, 1, 256, 256, ("gauss", 9, 1.5), 0.01, 0.05, 12, False, False, {"FUSED_ADJ": 0}),
+    ("fused-256-psf-K25", 2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, False, False, {}),
+    ("fused-256-c5layer-K50", 2, 3, 256, 256, None, 0.0041, 0.021, 50, False, False, {}),
+    ("generic-40x48-K6", 2, 1, 40, 48, ("gauss", 5, 1.0), 0.02, 0.1, 6, False, True, {}),
+    ("generic-29x37-rand-K8", 1, 2, 29, 37, ("rand", 7, 4), 0.0041, 0.021, 8, False, True, {}),
+    ("iso-32-K6", 20, 1, 32, 32, ("gauss", 5, 1.0), 0.02, 0.1, 6, True, True, {}),
+    ("iso-64-rand-K10", 2, 3, 64, 64, ("rand", 7, 4), 0.0041, 0.021, 10, True, True, {}),
+    ("iso-256-c2-K25", 2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, True, True, {}),
+    ("iso-256-c5layer-K50", 2, 3, 256, 256, None, 0.0041, 0.021, 50, True, False, {}),
+    ("iso-generic-45x36-K6", 3, 1, 45, 36, ("gauss", 5, 1.0), 0.02, 0.1, 6, True, True, {}),
+    # the reference demo's shape (src/ADMM_Deconv.jl:17-23): 32x32x3x2, a 32x32 PSF, K = 50
+    ("demo-32-psf32-K50", 2, 3, 32, 32, ("rand", 32, 32), 0.05, 0.3, 50, False, True, {}),
+    ("generic-40x30-psf40x30-K9", 2, 1, 30, 40, ("rand", 40, 30), 0.02, 0.1, 9, False, True, {}),
+]
+
+
+def _psf(spec, rng):
+    if spec is None:
+        return None
+    if spec[0] == "gauss":
+        return synth.gaussian_psf(spec[1], spec[2])
+    h = rng.random((spec[2], spec[1])).astype(np.float32)
+    return (h / h.sum()).astype(np.float32)
+
+
+def _devtest():
+    path = os.path.join(PKG_DIR, "libadmm_devtest.so")
+    if not os.path.exists(path):
+        pytest.fail("libadmm_devtest.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    f = lib.devtest_recording_offsets
+    f.argtypes = [ctypes.c_int] * 8 + [ctypes.POINTER(ctypes.c_size_t)] * 2
+    f.restype = ctypes.c_int
+    return f
+
+
+def lane_native_to_natural(a, planes):
+    """Fused-kernel trajectory slots (K-1, planes, 64 registers, 512 threads, 4) -> (K-1, planes, 2, 256, 256).
+    Entry [n][t = 2r + h] = (s0[p], s0[p+1], s1[p], s1[p+1]) of pixel pair p = 4n + 2h of line r
+    (plane_api.hpp): channel 0 = x - x(line r-1), channel 1 = x - x(pixel p-1)."""
+    a = a.reshape(-1, planes, 64, 256, 2, 2, 2)               # [k][plane][n][r][h][ch][e]
+    a = a.transpose(0, 1, 5, 3, 2, 4, 6)                        # [k][plane][ch][r][n][h][e]
+    return a.reshape(-1, planes, 2, 256, 256)
+
+
+def read_trajectory(rec, K, lane_native):
+    """(s_1..s_{K-1} as (K-1, B, P, 2, N, M) fp32, |s_k| maps (K-1, N, M) or None) of a recording."""
+    M, N, P, B, kh, kw = rec.dims
+    planes = B * P
+    ts, tn = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    assert _devtest()(M, N, P, B, kh, K, int(rec.want_h), int(rec.iso), ctypes.byref(ts), ctypes.byref(tn)) == 0
+    buf = rec.workspace._buf
+    ptr, _ = rec.workspace.get(0, buf.device)
+    base = ptr - buf.data_ptr()
+    n = (K - 1) * planes * 2 * M * N
+    s = buf[base + ts.value: base + ts.value + 4 * n].view(torch.float32).cpu().numpy()
+    if lane_native:
+        s = lane_native_to_natural(s, planes)
+    s = s.reshape(K - 1, B, P, 2, N, M)
+    nrm = None
+    if rec.iso:
+        m = (K - 1) * M * N
+        nrm = buf[base + tn.value: base + tn.value + 4 * m].view(torch.float32).cpu().numpy().reshape(K - 1, N, M)
+    return s, nrm
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _plane_rel(a, b):
+    a = np.asarray(a, np.float64).reshape(-1, a.shape[-2] * a.shape[-1])
+    b = np.asarray(b, np.float64).reshape(a.shape)
+    return max(_rel(a[i], b[i]) for i in range(a.shape[0]))
+
+
+def _scalar_rel(a, b):
+    if a == 0.0 and b == 0.0:   # K = 1: tau never enters the output
+        return 0.0
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_adjoint_vs_mask_conditioned_oracle(dev, case):
+    cid, B, P, N, M, spec, lam, rho, K, iso, need_h, opts = case
+    rng = np.random.default_rng(N + M + K + 31 * B)
+    h = _psf(spec, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=7)
+    xbar = rng.standard_normal(y.shape).astype(np.float32)
+    yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    with contextlib.ExitStack() as st:
+        for k, v in opts.items():
+            st.enter_context(_lib.option(k, v))
+        lane_native = (M == 256 and N == 256 and not iso and not (need_h and h is not None)
+                       and _lib.get_option("FUSED") == 1)
+        x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, iso, K, need_h=need_h)
+        torch.cuda.synchronize()
+        masks = []
+        if K > 1:
+            s_traj, nrm = read_trajectory(rec, K, lane_native)
+            masks = oracle_torch.masks_from_trajectory(s_traj, lam, rho, iso, nrm)
+        yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt)
+        torch.cuda.synchronize()
+    x0, yb0, hb0, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho),
+                                                        None if h is None else h.astype(np.float64), iso, K, xbar,
+                                                        masks=masks)
+    err = {"x": _plane_rel(x.cpu().numpy(), x0), "y_bar": _plane_rel(yb.cpu().numpy(), yb0),
+           "lambda_bar": _scalar_rel(float(lb), lb0), "rho_bar": _scalar_rel(float(rb), rb0)}
+    if hb is not None:
+        err["h_bar"] = _rel(hb.cpu().numpy(), hb0)
+    # the masks' distance from the oracle's own fp64 forward: how many bits the conditioning moved
+    if K > 1:
+        rec64 = []
+        oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)), torch.tensor(float(np.float32(lam)), dtype=torch.float64),
+                                   torch.tensor(float(np.float32(rho)), dtype=torch.float64),
+                                   None if h is None else torch.from_numpy(h.astype(np.float64)), iso, K, record=rec64)
+        own = oracle_torch.masks_from_trajectory(np.stack([r[0].numpy() for r in rec64]), lam, rho, iso,
+                                                 np.stack([r[1].numpy() for r in rec64]))
+        err["mask_flips_vs_fp64_forward"] = int(sum(np.sum((a[0] if not iso else a) != (b[0] if not iso else b))
+                                                    for a, b in zip(masks, own)))
+    out = os.environ.get("ADMM_GRAD_LOG")
+    if out:
+        with open(os.path.join(REPO, out), "a") as f:
+            f.write(json.dumps({"case": cid, **{k: (float(v) if not isinstance(v, int) else v) for k, v in err.items()}})
+                    + "\n")
+    for k in ("x", "y_bar", "lambda_bar", "rho_bar", "h_bar"):
+        if k in err:
+            assert err[k] <= TOL, f"{cid}: {k} relative error {err[k]:.3e} > {TOL} ({err})"

@@ -89,16 +89,18 @@ def test_parallel_branches_on_streams_match_serial(dev):
     assert all(torch.equal(a, b) for a, b in zip(l1, l2))
 
 
-def test_c5_denoiser_branch_gradients(dev):
+@pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])
+def test_c5_denoiser_branch_gradients(dev, iso):
     """BASELINE c5's caller: the get_denoiser branch of src/nets/net_build.jl:113-128 -- Parallel(chcat) of
-    5 x ADMMDeconvF2((), 50, rho, relu1) -- on a small RGB batch, branches on their own HIP streams.  The
-    gradient of a weighted sum of the output w.r.t. every branch's trainable lambda (deconv_admm.jl:107)
-    against fp64 autograd of the oracle: for branch i, lambda_bar = <xbar_i, d x_i / d lambda> with
-    xbar_i = w_i * relu1'(x_i)."""
+    5 x ADMMDeconvF2((), 50, rho, relu1, iso=use_iso) -- on a small RGB batch (2 x 3 planes of 256^2),
+    branches on their own HIP streams; iso = true is the training default (src/configs/train_cfg.json:14),
+    where the batch norm couples the 6 planes of a branch.  The gradient of a weighted sum of the output
+    w.r.t. every branch's trainable lambda (deconv_admm.jl:107) against fp64 autograd of the oracle: for
+    branch i, lambda_bar = <xbar_i, d x_i / d lambda> with xbar_i = w_i * relu1'(x_i)."""
     import oracle_torch
     rng = np.random.default_rng(12)
     rhos = (0.002, 0.02, 0.2, 2.0, 4.0)
-    br = [layers.ADMMDeconvF2((), 50, r, layers.relu1, rng=rng, device=dev) for r in rhos]
+    br = [layers.ADMMDeconvF2((), 50, r, layers.relu1, iso=iso, rng=rng, device=dev) for r in rhos]
     for L in br:
         L.lam.requires_grad_(True)
     net = layers.Parallel(layers.chcat, *br)
@@ -109,11 +111,45 @@ def test_c5_denoiser_branch_gradients(dev):
     torch.cuda.synchronize()
     for i, (L, r) in enumerate(zip(br, rhos)):
         lam = float(L.lam.detach().cpu()[0])
-        x0, _, _, lb0, _ = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(r), None,
-                                                      False, 50, np.zeros(y.shape, np.float32))
+        x0 = oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)),
+                                        torch.tensor(float(np.float32(lam)), dtype=torch.float64),
+                                        torch.tensor(float(np.float32(r)), dtype=torch.float64), None, iso, 50).numpy()
         xbar = w[:, 3 * i:3 * i + 3] * ((x0 > 0) & (x0 < 1))
         _, _, _, lb0, _ = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(r), None,
-                                                     False, 50, xbar.astype(np.float32))
+                                                     iso, 50, xbar.astype(np.float32))
         got = float(L.lam.grad.cpu()[0])
         assert abs(got - lb0) <= 5e-3 * abs(lb0), f"branch {i} (rho {r}): lambda_bar {got} vs {lb0}"
         np.testing.assert_allclose(out[:, 3 * i:3 * i + 3].detach().cpu().numpy(), np.clip(x0, 0, 1), atol=2e-4)
+
+
+def test_reference_demo_layer_forward_and_gradients(dev):
+    """The reference's own demo (src/ADMM_Deconv.jl:17-23): ADMMDeconv((32,32), 50, relu6) on a (32,32,3,2)
+    batch of crops -- a PSF as large as the image -- forward and the gradients of every trainable (PSF, lambda,
+    rho) and of the input, against fp64 autograd of the oracle through the same projection and relu6."""
+    import oracle_torch
+    rng = np.random.default_rng(17)
+    L = layers.ADMMDeconv((32, 32), 50, layers.relu6, rng=rng, device=dev)
+    for t in (L.weight, L.lam, L.rho):
+        t.requires_grad_(True)
+    y = synth.make_batch(2, 32, 32, synth.gaussian_psf(5, 1.0), P=3, g0=40)
+    w = rng.standard_normal(y.shape).astype(np.float32)
+    yt = torch.from_numpy(y).to(dev).requires_grad_(True)
+    out = L(yt)
+    (out * torch.from_numpy(w).to(dev)).sum().backward()
+    torch.cuda.synchronize()
+    h = L.weight.detach().cpu().numpy().reshape(32, 32).astype(np.float64)   # projected to [0, 1] (:219)
+    lam, rho = L.lam.item(), L.rho.item()
+    x0 = oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)), torch.tensor(lam, dtype=torch.float64),
+                                    torch.tensor(rho, dtype=torch.float64), torch.from_numpy(h), False, 50).numpy()
+    got = out.detach().cpu().numpy()
+    assert np.abs(got - np.clip(x0, 0, 6)).max() <= 2e-4 * max(1.0, np.abs(x0).max())
+    xbar = w * ((x0 > 0) & (x0 < 6))
+    _, yb0, hb0, lb0, rb0 = oracle_torch.tvd_fft_grads(y.astype(np.float64), np.float32(lam), np.float32(rho), h,
+                                                       False, 50, xbar)
+
+    def rel(a, b):
+        return float(np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b))
+    assert rel(yt.grad.cpu().numpy(), yb0) < 1e-3
+    assert rel(L.weight.grad.cpu().numpy().reshape(32, 32), hb0) < 1e-3
+    assert abs(float(L.lam.grad) - lb0) <= 1e-3 * abs(lb0)
+    assert abs(float(L.rho.grad) - rb0) <= 1e-3 * abs(rb0)

@@ -99,3 +99,22 @@ def test_deterministic(dev):
         (metrics.gmsd(xt, yt) + metrics.ssim_loss(xt, yt)).backward()
         grads.append(xt.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_gmsd_on_two_streams_does_not_share_scratch(dev):
+    """Two GMSD calls enqueued on two streams at once (the c5 branches' losses could be) each get their own
+    scratch: the results equal the same calls made one after the other on the default stream."""
+    shapes = [(2, 3, 128, 96), (4, 1, 200, 160)]   # different sizes: the second would grow a shared buffer
+    pairs = [tuple(torch.from_numpy(a).to(dev) for a in _pair(s, 10 + i)) for i, s in enumerate(shapes)]
+    ref = [metrics.gmsd(x, y, reduction=lambda v: v) for x, y in pairs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in pairs]
+    got = [None, None]
+    for rep in range(5):
+        for i, ((x, y), st) in enumerate(zip(pairs, streams)):
+            st.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(st):
+                got[i] = metrics.gmsd(x, y, reduction=lambda v: v)
+        torch.cuda.synchronize()
+        for g, r in zip(got, ref):
+            assert torch.equal(g, r)

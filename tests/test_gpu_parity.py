@@ -41,6 +41,9 @@ CASES = [
     (2, 1, 128, 128, ("box",), 0.0041, 0.021, 100),            # reference test PSF, default maxit
     (1, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 1),
     (1, 1, 64, 64, ("gauss", 9, 1.2), 0.0041, 0.021, 2),
+    # the reference's demo, ADMMDeconv((32,32), 50, relu6) on (32,32,3,2) crops (src/ADMM_Deconv.jl:17-23):
+    # the PSF is as large as the image (kh = M, kw = N; padd = 15 wraps the whole plane)
+    (2, 3, 32, 32, ("rand", 32, 32), 0.05, 0.3, 50),
 ]
 
 
@@ -80,6 +83,7 @@ GENERIC_CASES = [
     (1, 1, 480, 640, ("gauss", 15, 2.5), 0.0041, 0.021, 5, False),  # a photograph
     (20, 1, 40, 24, ("gauss", 5, 1.0), 0.02, 0.1, 6, True),         # isotropic, two plane groups
     (2, 3, 33, 50, None, 0.05, 0.1, 7, True),
+    (2, 1, 30, 40, ("rand", 40, 30), 0.02, 0.1, 9, False),        # PSF as large as the image (kh = M, kw = N)
 ]
 
 

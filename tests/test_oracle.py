@@ -113,3 +113,43 @@ def test_golden_fixture_reproduces(path):
     if p["M"] * p["N"] <= 64 * 128:
         c = oracle_c.tvd_fft_c(d["y"], p["lam"], p["rho"], h, p["iso"], p["K"], np.float64, nthreads=2)
         assert np.abs(c - d["x"]).max() <= 1e-6 * max(1.0, np.abs(c).max())
+
+
+@pytest.mark.parametrize("iso", [False, True])
+def test_mask_conditioned_oracle_equals_oracle_on_its_own_masks(iso):
+    """The gradient oracle with the prox branches held at the masks of its OWN fp64 forward is the plain
+    oracle (the masked prox is the exact prox there), bitwise in x and to fp64 rounding in every gradient;
+    with one mask bit flipped it is not (the conditioning has an effect)."""
+    import torch
+    import oracle_torch as ot
+    from admm_deconv import synth
+    rng = np.random.default_rng(4)
+    h = synth.gaussian_psf(5, 1.0)
+    y = synth.make_batch(2, 24, 20, h, P=1).astype(np.float64)
+    xbar = rng.standard_normal(y.shape)
+    lam, rho, K = np.float32(0.02), np.float32(0.1), 6
+    rec = []
+    ot.tvd_fft_torch(torch.from_numpy(y), torch.tensor(float(lam), dtype=torch.float64),
+                     torch.tensor(float(rho), dtype=torch.float64), torch.from_numpy(h.astype(np.float64)), iso, K,
+                     record=rec)
+    assert len(rec) == K - 1
+    s_traj = np.stack([r[0].numpy() for r in rec])
+    n_traj = np.stack([r[1].numpy() for r in rec])
+    masks = ot.masks_from_trajectory(s_traj, lam, rho, iso, n_traj)
+    a = ot.tvd_fft_grads(y, lam, rho, h.astype(np.float64), iso, K, xbar)
+    b = ot.tvd_fft_grads(y, lam, rho, h.astype(np.float64), iso, K, xbar, masks=masks)
+    assert np.allclose(a[0], b[0], rtol=0, atol=1e-13)
+    for u, v in zip(a[1:], b[1:]):
+        assert np.allclose(u, v, rtol=1e-10, atol=1e-13)
+    # flip the mask of one pixel of iteration 2
+    m0 = masks[1][0] if not iso else masks[1]
+    flip = np.unravel_index(np.argmax(m0), m0.shape)
+    if iso:
+        masks[1] = masks[1].copy()
+        masks[1][flip] = 0.0
+    else:
+        m, sg = masks[1][0].copy(), masks[1][1]
+        m[flip] = 0.0
+        masks[1] = (m, sg)
+    c = ot.tvd_fft_grads(y, lam, rho, h.astype(np.float64), iso, K, xbar, masks=masks)
+    assert not np.allclose(a[1], c[1], rtol=1e-8, atol=1e-12)
