@@ -36,7 +36,13 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_tvd_forward_dev_f32", "admm_tvd_backward_dev_f32", "admm_tvd_forward_record_dev_f32",
            "admm_tvd_backward_recorded_dev_f32", "admm_set_option", "admm_get_option",
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
-           "admm_profile_enable", "admm_profile_reset", "admm_profile_get")
+           "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
+           "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
+           "admm_tvd_backward_multi_recorded_dev_f32")
+
+# record flags (the want_hbar word of the record entry points) and multi-branch flags
+REC_HBAR, REC_MASKS = 1, 2
+MULTI_RECORD = 1
 
 
 # admm_reduce_fn / admm_batch_reducer (include/admm_deconv.h): cross-shard sum of an M x N map
@@ -111,6 +117,14 @@ def load():
                                                   c_void_p, ctypes.POINTER(BatchReducer)]
     L.admm_tvd_backward_recorded_dev_f32.restype = c_int
     L.admm_tvd_backward_recorded_dev_f32.argtypes = list(L.admm_tvd_backward_dev_f32.argtypes)
+    L.admm_tvd_multi_workspace_bytes.restype = c_int
+    L.admm_tvd_multi_workspace_bytes.argtypes = [c_int] * 7 + [ctypes.POINTER(c_size_t)]
+    L.admm_tvd_forward_multi_dev_f32.restype = c_int
+    L.admm_tvd_forward_multi_dev_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 5 + [
+        ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p), c_int, c_int, c_void_p, c_size_t, c_void_p]
+    L.admm_tvd_backward_multi_recorded_dev_f32.restype = c_int
+    L.admm_tvd_backward_multi_recorded_dev_f32.argtypes = [c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_void_p,
+                                                                                          c_size_t, c_void_p]
     L.admm_set_option.restype = c_int
     L.admm_set_option.argtypes = [c_int, c_int]
     L.admm_get_option.restype = c_int
@@ -149,9 +163,17 @@ def workspace_bytes(M, N, P, B, kh, kw, iso):
 
 
 def backward_workspace_bytes(M, N, P, B, kh, kw, iso, maxit, want_hbar):
+    """want_hbar: a bool (h_bar wanted) or the flag word REC_HBAR | REC_MASKS."""
     out = ctypes.c_size_t(0)
-    check(load().admm_tvd_backward_workspace_bytes(M, N, P, B, kh, kw, int(bool(iso)), int(maxit),
-                                                   int(bool(want_hbar)), ctypes.byref(out)))
+    flags = int(want_hbar)
+    check(load().admm_tvd_backward_workspace_bytes(M, N, P, B, kh, kw, int(bool(iso)), int(maxit), flags,
+                                                   ctypes.byref(out)))
+    return out.value
+
+
+def multi_workspace_bytes(M, N, P, B, nbranch, maxit, flags):
+    out = ctypes.c_size_t(0)
+    check(load().admm_tvd_multi_workspace_bytes(M, N, P, B, nbranch, int(maxit), int(flags), ctypes.byref(out)))
     return out.value
 
 

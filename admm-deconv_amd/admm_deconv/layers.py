@@ -24,7 +24,7 @@ import math
 import numpy as np
 import torch
 
-from .ops import tvd_fft
+from .ops import multi_supported, tvd_fft, tvd_fft_multi_grad
 
 __all__ = ["ADMMDeconv", "ADMMDeconvF1", "ADMMDeconvF2", "ADMMDeconvF3", "Admm", "Parallel", "chcat",
            "glorot_uniform", "identity", "relu", "relu6", "relu1"]
@@ -210,17 +210,48 @@ class Parallel:
     """Flux `Parallel(connection, layers...)` as the nets build it (net_build.jl:121-125, :175): every
     branch sees the same input and `connection` combines the branch outputs.
 
-    The branches are independent, so on a ROCm device each runs on its own HIP stream (forward, and --
-    autograd replays a backward op on its forward's stream -- the adjoint too), then the caller's stream
-    waits for all of them.  One ADMM layer's per-plane kernels occupy one CU per plane (192 of 256 CUs
-    for the c5 batch of 64 RGB images); concurrent branches fill the rest.  streams=False runs the
+    When every branch is an ADMM layer the one-grid solve covers (the denoiser: ADMMDeconvF2((), K, ρ_i, σ),
+    anisotropic, 256 x 256, same K), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
+    planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
+    each branch's bias and σ then apply to its slice.  Results are bitwise those of the branches run one
+    by one.  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
+    (forward, and -- autograd replays a backward op on its forward's stream -- the adjoint too), then the
+    caller's stream waits for all of them.  merge=False keeps the per-branch path; streams=False runs the
     branches one after the other on the caller's stream (the reference's single task-local stream)."""
 
-    def __init__(self, connection, *layers, streams=True):
+    def __init__(self, connection, *layers, streams=True, merge=True):
         self.connection = connection
         self.layers = list(layers)
         self.use_streams = bool(streams)
+        self.merge = bool(merge)
         self._streams = {}
+
+    def _mergeable(self, x):
+        if not self.merge or len(self.layers) < 2:
+            return False
+        Ls = self.layers
+        if not all(isinstance(L, Admm) for L in Ls):
+            return False
+        K = Ls[0].iters
+        return all(L.iters == K and not L.iso and L.weight.numel() == 0 and L.group is None for L in Ls) and \
+            multi_supported(x)
+
+    def _merged(self, x):
+        """All branches in one solve (ops.tvd_fft_multi); bias and σ per branch, then the connection."""
+        Ls = self.layers
+        for L in Ls:
+            L.project()          # deconv_admm.jl:216-219, in place on the device
+        xa = tvd_fft_multi_grad(x, [L.lam for L in Ls], [L.rho for L in Ls], Ls[0].iters)
+        P = x.shape[1]
+        if self.connection is chcat and all(L.bias is False and L.sigma is Ls[0].sigma for L in Ls):
+            return Ls[0].sigma(xa)   # σ elementwise over the whole chcat tensor: the same values, no copies
+        outs = []
+        for i, L in enumerate(Ls):
+            o = xa[:, i * P:(i + 1) * P]
+            if L.bias is not False:
+                o = o + L.bias
+            outs.append(L.sigma(o))
+        return self.connection(*outs)
 
     def _side_streams(self, dev):
         if dev not in self._streams:
@@ -228,6 +259,8 @@ class Parallel:
         return self._streams[dev]
 
     def __call__(self, x):
+        if self._mergeable(x):
+            return self._merged(x)
         if not (self.use_streams and isinstance(x, torch.Tensor) and x.is_cuda and len(self.layers) > 1):
             return self.connection(*[L(x) for L in self.layers])
         cur = torch.cuda.current_stream(x.device)

@@ -19,7 +19,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["tvd_fft", "tvd_fft_backward", "tvd_fft_record", "tvd_fft_backward_recorded", "Recording", "Workspace"]
+__all__ = ["tvd_fft", "tvd_fft_backward", "tvd_fft_record", "tvd_fft_backward_recorded", "Recording", "Workspace",
+           "tvd_fft_multi", "tvd_fft_multi_backward_recorded", "multi_supported"]
 
 
 class Workspace:
@@ -283,12 +284,17 @@ class Recording:
     once (no recompute in the backward).  Memory: about 8 B/px per iteration (plus 8 B/px of dim-2
     spectra per iteration with a PSF when h_bar is needed) -- sized for MI355X's 288 GB HBM."""
 
-    __slots__ = ("workspace", "y4", "hb", "shape", "dv", "lam", "rho", "iso", "maxit", "want_h", "group", "dims")
+    __slots__ = ("workspace", "y4", "hb", "shape", "dv", "lam", "rho", "iso", "maxit", "want_h", "group", "dims",
+                 "flags")
 
 
-def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, stream=None, group=None):
+def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_h=True, need_rho=True, stream=None,
+                   group=None):
     """Forward solve that records its trajectory.  Returns (x, Recording); see tvd_fft_backward_recorded.
-    lam / rho as device tensors are read in-kernel (no host sync), as in tvd_fft."""
+    lam / rho as device tensors are read in-kernel (no host sync), as in tvd_fft.  need_rho=False: the
+    replay will not be asked for rho_bar, so the fused 256 x 256 anisotropic path records only the
+    soft-threshold branch of every trajectory element (ADMM_REC_MASKS: 16x less memory, a cheaper reverse
+    sweep, the other gradients bitwise the same)."""
     shape, y4, hb = _prep(y, h)
     B, P, N, M = y4.shape
     stream, s_handle = _stream_of(stream, y.device)
@@ -298,13 +304,14 @@ def tvd_fft_record(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, need_
     rec.want_h = bool(need_h and hb is not None)
     rec.y4, rec.hb, rec.shape, rec.iso, rec.maxit, rec.group = y4, hb, shape, bool(isotropic), int(maxit), group
     rec.dims = (M, N, P, B, kh, kw)
-    nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, rec.want_h)
+    rec.flags = (_lib.REC_HBAR if rec.want_h else 0) | (0 if need_rho else _lib.REC_MASKS)
+    nbytes = _lib.backward_workspace_bytes(M, N, P, B, kh, kw, isotropic, maxit, rec.flags)
     rec.workspace = Workspace()
     ws_ptr, ws_len = rec.workspace.get(nbytes, y.device, stream)
     x = torch.empty_like(y4)
     red, keep = _make_reducer(rec.workspace, group) if _sharded(isotropic, group) else (None, None)
     head = (y4.data_ptr(), x.data_ptr(), M, N, P, B, None if hb is None else hb.data_ptr(), kh, kw)
-    tail = (int(rec.iso), rec.maxit, int(rec.want_h), ws_ptr, ws_len, s_handle,
+    tail = (int(rec.iso), rec.maxit, rec.flags, ws_ptr, ws_len, s_handle,
             ctypes.byref(red) if red is not None else None)
     L = _lib.load()
     if rec.dv is not None:
@@ -363,8 +370,9 @@ class _TvdFFTFn(torch.autograd.Function):
         # (device tensors) are read in-kernel unless the caller handed their host values in `scalars`
         need_h = h_t.numel() > 0 and ctx.needs_input_grad[3]
         lam, rho = scalars if scalars is not None else (lam_t, rho_t)
+        # rho not trainable here (ADMMDeconvF2, F3): the recording keeps only the ST branches when it can
         x, ctx.rec = tvd_fft_record(y, lam, rho, h_t if h_t.numel() else None, isotropic, maxit,
-                                    need_h=need_h, group=group)
+                                    need_h=need_h, need_rho=ctx.needs_input_grad[2], group=group)
         # y (read again by the reverse sweep's h_bar correlation) and x are version-checked: an in-place
         # change of either between forward and backward raises instead of giving a wrong gradient
         ctx.save_for_backward(y, lam_t, rho_t, h_t, x)
@@ -411,3 +419,122 @@ def tvd_fft(y, lam, rho=1.0, h=None, isotropic=False, maxit=100, *, out=None, wo
     if scalars is not None:
         lam, rho = scalars
     return _forward_raw(y, lam, rho, h, isotropic, maxit, out=out, workspace=workspace, stream=stream, group=group)
+
+
+# ---- several ADMM branches of one shared input (Parallel(chcat, ...), src/nets/net_build.jl:113-125) ----
+MULTI_M = MULTI_N = 256
+
+
+def multi_supported(y, isotropic=False, psf=None, group=None):
+    """Whether the one-grid multi-branch solve (admm_tvd_forward_multi_dev_f32) covers this input: the fused
+    256 x 256 anisotropic kernel, no PSF, one process holding the batch, and the fused option on."""
+    return (isinstance(y, torch.Tensor) and y.is_cuda and y.dtype == torch.float32 and y.dim() == 4
+            and y.shape[-1] == MULTI_M and y.shape[-2] == MULTI_N and not isotropic
+            and (psf is None or psf.numel() == 0) and group is None and _lib.get_option("FUSED") == 1)
+
+
+class MultiRecording:
+    """A multi-branch forward recorded for its reverse sweep (tvd_fft_multi(record=True))."""
+    __slots__ = ("workspace", "dims", "maxit", "masks", "dv")
+
+
+def _ptr_array(ts):
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def tvd_fft_multi(y, lams, rhos, maxit=100, *, out=None, record=False, need_rho=True, workspace=None, stream=None):
+    """x = chcat(tvd_fft(y, lams[0], rhos[0], nothing, false, maxit), ..., tvd_fft(y, lams[n-1], ...)) in ONE
+    launch of the fused kernel (every branch's planes in one grid).  y: (B, P, 256, 256) float32 on the
+    device; lams, rhos: n 1-element tensors / numbers (device tensors read in-kernel).  Returns x of shape
+    (B, n * P, 256, 256) -- the chcat layout, branch i's channels at i*P..i*P+P-1 -- and, with record=True,
+    a MultiRecording for tvd_fft_multi_backward_recorded (need_rho=False: only the ST branches are kept)."""
+    if not multi_supported(y):
+        raise ValueError("tvd_fft_multi: y must be a float32 (B, P, 256, 256) ROCm tensor (fused option on)")
+    n = len(lams)
+    if n < 1 or len(rhos) != n:
+        raise ValueError("tvd_fft_multi: one lambda and one rho per branch")
+    y4 = y.contiguous()
+    B, P, N, M = y4.shape
+    stream, s_handle = _stream_of(stream, y.device)
+    dv = [_DevScalars(l, r, y.device, stream) for l, r in zip(lams, rhos)]
+    flags = (_lib.MULTI_RECORD | (0 if need_rho else _lib.REC_MASKS)) if record else 0
+    nbytes = _lib.multi_workspace_bytes(M, N, P, B, n, maxit, flags)
+    if record:
+        workspace = Workspace()
+    elif workspace is None:
+        workspace = _default_workspace("multi", y.device, stream)
+    ws_ptr, ws_len = workspace.get(nbytes, y.device, stream)
+    if out is None:
+        out = torch.empty((B, n * P, N, M), dtype=torch.float32, device=y.device)
+    elif out.shape != (B, n * P, N, M) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (B, n*P, N, M) float32 tensor")
+    lp, rp = _ptr_array([d.lam for d in dv]), _ptr_array([d.rho for d in dv])
+    _lib.check(_lib.load().admm_tvd_forward_multi_dev_f32(y4.data_ptr(), out.data_ptr(), M, N, P, B, n, lp, rp,
+                                                          int(maxit), flags, ws_ptr, ws_len, s_handle))
+    if not record:
+        return out
+    rec = MultiRecording()
+    rec.workspace, rec.dims, rec.maxit, rec.masks, rec.dv = workspace, (M, N, P, B, n), int(maxit), not need_rho, dv
+    return out, rec
+
+
+def tvd_fft_multi_backward_recorded(rec, x, x_bar, *, need_y=True, need_rho=True, stream=None):
+    """Reverse sweep of a recorded multi-branch forward (x = its output, unmodified; x_bar in x's chcat
+    layout).  Returns (y_bar or None, lam_bar (n,), rho_bar (n,) or None); y_bar sums the branches' input
+    gradients.  Consumes the recording."""
+    if rec.workspace is None:
+        raise RuntimeError("recording already consumed")
+    M, N, P, B, n = rec.dims
+    if need_rho and rec.masks:
+        raise ValueError("recorded with need_rho=False: rho_bar is not available")
+    stream, s_handle = _stream_of(stream, x.device)
+    xb = x_bar.reshape(x.shape).to(torch.float32).contiguous()
+    ws_ptr, ws_len = rec.workspace.get(0, x.device, stream)
+    y_bar = torch.empty((B, P, N, M), dtype=torch.float32, device=x.device) if need_y else None
+    scal = torch.zeros(2 * n, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.load().admm_tvd_backward_multi_recorded_dev_f32(
+        xb.data_ptr(), y_bar.data_ptr() if need_y else None, scal.data_ptr(),
+        scal.data_ptr() + 4 * n if need_rho else None, M, N, P, B, n, rec.maxit, x.data_ptr(), ws_ptr, ws_len,
+        s_handle))
+    rec.workspace = None
+    return y_bar, scal[:n], scal[n:] if need_rho else None
+
+
+class _TvdFFTMultiFn(torch.autograd.Function):
+    """Differentiable tvd_fft_multi: one recorded forward of every branch, one reverse sweep."""
+
+    @staticmethod
+    def forward(ctx, y, maxit, n, *params):
+        lams, rhos = params[:n], params[n:]
+        ctx.n = n
+        need_rho = any(ctx.needs_input_grad[3 + n + i] for i in range(n))
+        x, ctx.rec = tvd_fft_multi(y, lams, rhos, maxit, record=True, need_rho=need_rho)
+        ctx.need_rho = need_rho
+        ctx.save_for_backward(y, x, *params)
+        return x
+
+    @staticmethod
+    def backward(ctx, x_bar):
+        y, x, *params = ctx.saved_tensors
+        n = ctx.n
+        yb, lb, rb = tvd_fft_multi_backward_recorded(ctx.rec, x, x_bar, need_y=ctx.needs_input_grad[0],
+                                                     need_rho=ctx.need_rho)
+        ctx.rec = None
+        grads = [yb if ctx.needs_input_grad[0] else None, None, None]
+        for i in range(n):
+            p = params[i]
+            grads.append(lb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[3 + i] else None)
+        for i in range(n):
+            p = params[n + i]
+            grads.append(rb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[3 + n + i] else None)
+        return tuple(grads)
+
+
+def tvd_fft_multi_grad(y, lams, rhos, maxit=100):
+    """tvd_fft_multi under autograd when y or any lam / rho tensor requires grad (else the plain call)."""
+    ts = [t for t in (y, *lams, *rhos) if isinstance(t, torch.Tensor)]
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        dev = y.device
+        as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.full((1,), float(v), device=dev)  # noqa: E731
+        return _TvdFFTMultiFn.apply(y, int(maxit), len(lams), *[as_t(v) for v in lams], *[as_t(v) for v in rhos])
+    return tvd_fft_multi(y, lams, rhos, maxit)

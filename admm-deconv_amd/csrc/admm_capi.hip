@@ -350,6 +350,7 @@ struct Traj {
     float2* v = nullptr;     // K x planes x N x M/2        : forward dim-2 spectra (h_bar only)
     double2* sig = nullptr;  // (M/2+1) x N                 : top-left PSF spectrum (h_bar only)
     float* nrm = nullptr;    // (K-1) x M x N               : isotropic batch norm of s_k (iso only)
+    unsigned* m = nullptr;   // (K-1) x planes x 16 x 512   : ST mask bytes of s_k instead of s (fused only)
 };
 
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
@@ -458,7 +459,8 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         if (rc) return rc;
         rc = ln.run(ADMM_K_PLANE, [&] {
             return pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
-                                   planes, s, reinterpret_cast<float4*>(tr.s), opt(ADMM_OPT_PLANE_STAGGER));
+                                   planes, s, tr.m ? nullptr : reinterpret_cast<float4*>(tr.s),
+                                   opt(ADMM_OPT_PLANE_STAGGER), nullptr, tr.m);
         });
         return rc;
     }
@@ -715,9 +717,10 @@ struct BwdLayout {
 constexpr int kIsoAdjRBlocks = 256;     // ISO_ADJ_R grid (tau_bar partial rows per step)
 constexpr int kRedParts = 256;          // first-stage blocks per column of a long column sum
 
-BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h, bool iso) {
+BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit, bool want_h, bool iso,
+                          bool masks = false) {
     BwdLayout b{};
-    const BwdHead hd = bwd_head(M, N, planes, kh, maxit, want_h, iso);
+    const BwdHead hd = bwd_head(M, N, planes, kh, maxit, want_h, iso, masks);
     b.f = hd.f;
     b.traj_s = hd.traj_s, b.traj_v = hd.traj_v, b.sig = hd.sig, b.sbA = hd.sbA, b.sbB = hd.sbB, b.vsum = hd.vsum;
     b.traj_n = hd.traj_n;
@@ -849,15 +852,19 @@ struct RecTag {
     // read without a synchronisation): a replay with other host values is refused
     float lam, rho;
     int dev_scalars;
+    int masks;   // the trajectory holds ST mask bytes (ADMM_REC_MASKS): no rho_bar
+    int nbr;     // branches of a multi-branch recording (1: a single solve)
     bool operator==(const RecTag& o) const { return std::memcmp(this, &o, sizeof(RecTag)) == 0; }
 };
 std::mutex g_rec_mu;
 std::unordered_map<const void*, RecTag> g_rec;
+float g_dummy_scalar = 0.f;   // stands for "device-resident scalars" when a tag is rebuilt without them
 
 RecTag make_tag(int M, int N, int P, int B, int kh, int kw, int iso, int maxit, bool want_h, const admm::ScalarSrc& sc) {
     RecTag t;
     std::memset(&t, 0, sizeof(t));
     t.M = M, t.N = N, t.P = P, t.B = B, t.kh = kh, t.kw = kw, t.iso = iso != 0, t.maxit = maxit, t.want_h = want_h;
+    t.nbr = 1;
     t.dev_scalars = sc.lam != nullptr;
     if (!t.dev_scalars) t.lam = sc.lam_v, t.rho = sc.rho_v;
     for (int i = 0; i < ADMM_OPT_COUNT; ++i) t.opts[i] = opt(i);
@@ -898,9 +905,9 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
 }
 
 // phases: 1 = forward recording the trajectory into the workspace (writes x_out), 2 = reverse sweep
-// from a recorded workspace (x_out = that forward's output), 3 = both.  want_hbar_rec: phase 1 alone
+// from a recorded workspace (x_out = that forward's output), 3 = both.  rec_flags (ADMM_REC_*): phase 1 alone
 // records the extra h_bar trajectory only when asked (phase 2 must then be given h_bar).
-int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_bar, float* y_bar, float* h_bar,
+int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, float* y_bar, float* h_bar,
                  float* lambda_bar, float* rho_bar, int M, int N, int P, int B, const float* h, int kh, int kw,
                  const admm::ScalarSrc& sc, int iso, int maxit, float* x_out, void* workspace, size_t workspace_bytes,
                  void* stream, const admm_batch_reducer* reducer) {
@@ -916,13 +923,23 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
-    const bool want_h = (phases == 1 ? want_hbar_rec != 0 : h_bar != nullptr) && kh > 0;
+    const bool want_h = (phases == 1 ? (rec_flags & ADMM_REC_HBAR) != 0 : h_bar != nullptr) && kh > 0;
     // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
     const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
-    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0);
+    // mask-bit trajectory (ADMM_REC_MASKS, fused forward + fused reverse sweep): asked for by a recording,
+    // and taken by the combined call whenever rho_bar is not wanted
+    const bool masks_ok = ln_traj && !iso && fused_adj_enabled();
+    bool use_masks = masks_ok && (phases == 1 ? (rec_flags & ADMM_REC_MASKS) != 0 : rho_bar == nullptr);
+    if (phases == 2) {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        auto it = g_rec.find(workspace);
+        use_masks = it != g_rec.end() && it->second.masks != 0;
+    }
+    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0, use_masks);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
-    const RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h, sc);
+    RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h, sc);
+    tag.masks = use_masks;
     if (phases == 2) {
         std::lock_guard<std::mutex> lk(g_rec_mu);
         auto it = g_rec.find(workspace);
@@ -932,6 +949,9 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
         if (!(it->second == tag))
             return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request, "
                                         "lambda / rho or library options changed between record and replay)");
+        if (use_masks && rho_bar)
+            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only): rho_bar cannot be "
+                                        "formed from it; record without the flag to get rho_bar");
         g_rec.erase(it);
     } else {
         std::lock_guard<std::mutex> lk(g_rec_mu);
@@ -970,6 +990,7 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     // ---- forward with trajectory ----
     Traj tr;
     tr.s = reinterpret_cast<float*>(ws + bl.traj_s);
+    tr.m = use_masks ? reinterpret_cast<unsigned*>(ws + bl.traj_s) : nullptr;
     tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
@@ -1012,8 +1033,9 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
             if (rc) return rc;
         }
         rc = ln.run(ADMM_K_ADJ, [&] {
-            return pk::launch_plane_adj(x_bar, ws + bl.f.F, reinterpret_cast<const float4*>(tr.s), dxK,
-                                       reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s);
+            return pk::launch_plane_adj(x_bar, ws + bl.f.F, tr.m ? static_cast<const void*>(tr.m) : tr.s, dxK,
+                                       reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s,
+                                       nullptr, tr.m != nullptr);
         });
         if (rc) return rc;
         red_rows = (int)planes;
@@ -1211,6 +1233,205 @@ int run_backward(int phases, int want_hbar_rec, const float* y, const float* x_b
     return ln.finish();
 }
 
+// ---- several branches of one shared input in one grid (Parallel(chcat, ...), net_build.jl:113-125) ----
+// Workspace: per branch {tau, rho, lambda} (16 B each, one block), its C table and its lane-native tables;
+// per grid plane the fused kernel's H^T y (= y) and s state, the trajectory (full s_k or mask bytes), the
+// reverse sweep's sbar and Vsum state and the (rho_bar, tau_bar) partials.  After the forward, the H^T y
+// slots hold each branch's Vsum (natural layout, y_bar only) and the s slots D x_K (rho_bar only).
+struct MultiLayout {
+    size_t prm, twM, twN, C, F, hln, sln, traj, sbar, vsl, part, rt, rtmp, total;
+};
+constexpr int kMultiM = 256, kMultiN = 256;
+size_t multi_C_bytes() { return align_up((size_t)(kMultiM / 2 + 1) * kMultiN * 4); }
+size_t multi_F_bytes() { return align_up(admm::plane::tables_bytes()); }
+
+MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
+    MultiLayout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        size_t o = off;
+        off = align_up(off + bytes);
+        return o;
+    };
+    const size_t MN = (size_t)kMultiM * kMultiN;
+    const int K = maxit < 1 ? 1 : maxit;
+    const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = (flags & ADMM_REC_MASKS) != 0;
+    L.prm = take((size_t)nbr * 16);
+    L.twM = take(kMultiM * 8);
+    L.twN = take(kMultiN * 8);
+    L.C = take((size_t)nbr * multi_C_bytes());
+    L.F = take((size_t)nbr * multi_F_bytes());
+    L.hln = take(planes * MN * 4);
+    L.sln = take(planes * MN * 8);
+    if (rec) {
+        L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 8 : MN * 8));
+        L.sbar = take(planes * MN * 8);
+        L.vsl = take(planes * MN * 4);
+        L.part = take(planes * 16);
+        L.rt = take((size_t)nbr * 16);
+        L.rtmp = take((size_t)kRedParts * 2 * 8);
+    }
+    L.total = off;
+    return L;
+}
+
+int check_multi(int M, int N, int P, int B, int nbr, int maxit, int flags) {
+    if (P < 1 || B < 1 || nbr < 1) return fail(ADMM_E_INVALID, "sizes must be positive (P=%d B=%d nbranch=%d)", P, B, nbr);
+    if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
+    if (flags & ~(ADMM_MULTI_RECORD | ADMM_REC_MASKS)) return fail(ADMM_E_INVALID, "unknown flags 0x%x", flags);
+    if (M != kMultiM || N != kMultiN || !fused_enabled())
+        return fail(ADMM_E_UNSUPPORTED, "the multi-branch solve is the fused 256 x 256 anisotropic kernel (got %d x %d%s); "
+                                        "solve the branches one by one", M, N, fused_enabled() ? "" : ", option FUSED = 0");
+    if ((size_t)P * B * nbr > kChunkPlanes)
+        return fail(ADMM_E_UNSUPPORTED, "at most %zu planes (nbranch * P * B) per multi-branch call", kChunkPlanes);
+    return ADMM_OK;
+}
+
+admm::plane::Branches multi_branches(int P, int B, int nbr) {
+    return admm::plane::Branches{P * B, nbr, P, (unsigned)(multi_F_bytes() / 4), 4u};
+}
+
+int forward_multi(const float* y, float* x_out, int M, int N, int P, int B, int nbr, const float* const* lambda,
+                  const float* const* rho, int maxit, int flags, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_multi(M, N, P, B, nbr, maxit, flags);
+    if (rc) return rc;
+    rc = check_common(y, x_out, maxit);
+    if (rc) return rc;
+    if (!lambda || !rho) return fail(ADMM_E_INVALID, "lambda and rho must be host arrays of nbranch device pointers");
+    for (int i = 0; i < nbr; ++i)
+        if (!lambda[i] || !rho[i]) return fail(ADMM_E_INVALID, "lambda[%d] / rho[%d] must be device pointers", i, i);
+    const size_t planes = (size_t)P * B * nbr;
+    const MultiLayout L = make_multi_layout(planes, nbr, maxit, flags);
+    rc = check_ws(workspace, workspace_bytes, L.total);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        g_rec.erase(workspace);
+        if (flags & ADMM_MULTI_RECORD) {
+            RecTag t = make_tag(M, N, P, B, 0, 0, 0, maxit, false, admm::ScalarSrc{lambda[0], rho[0], 0.f, 0.f});
+            t.nbr = nbr;
+            t.masks = (flags & ADMM_REC_MASKS) != 0;
+            g_rec[workspace] = t;
+        }
+    }
+    unsigned char* ws = static_cast<unsigned char*>(workspace);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    Launcher ln{s, g_prof.on, {}};
+    float* prm = reinterpret_cast<float*>(ws + L.prm);
+    float2* twM = reinterpret_cast<float2*>(ws + L.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + L.twN);
+    for (int i = 0; i < nbr; ++i) {
+        float* Ct = reinterpret_cast<float*>(ws + L.C + (size_t)i * multi_C_bytes());
+        void* F = ws + L.F + (size_t)i * multi_F_bytes();
+        const admm::ScalarSrc sc{lambda[i], rho[i], 0.f, 0.f};
+        rc = ln.run(ADMM_K_SETUP, [&] {
+            const size_t lds = (size_t)(M + N) * 16;
+            const int nb = (int)(((size_t)(M / 2 + 1) * N + kThreads - 1) / kThreads);
+            set_lds(admm::setup_kernel, lds);
+            hipLaunchKernelGGL(admm::setup_kernel, dim3(nb < 1024 ? nb : 1024), dim3(kThreads), lds, s, twM, twN, Ct,
+                               (float2*)nullptr, (const float*)nullptr, 0, 0, M, N, sc, prm + 4 * i, (double2*)nullptr);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_SETUP, [&] { return admm::plane::launch_tables(Ct, nullptr, F, s); });
+        if (rc) return rc;
+    }
+    if (maxit == 0) {
+        hipError_t e = hipMemsetAsync(x_out, 0, planes * (size_t)M * N * 4, s);
+        if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+        return ln.finish();
+    }
+    const admm::plane::Branches br = multi_branches(P, B, nbr);
+    const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = rec && (flags & ADMM_REC_MASKS) != 0;
+    rc = ln.run(ADMM_K_PLANE, [&] {
+        return admm::plane::launch_plane(y, x_out, ws + L.F, false, reinterpret_cast<float2*>(ws + L.hln),
+                                         reinterpret_cast<float4*>(ws + L.sln), prm, maxit, planes, s,
+                                         rec && !masks ? reinterpret_cast<float4*>(ws + L.traj) : nullptr,
+                                         opt(ADMM_OPT_PLANE_STAGGER), &br,
+                                         masks ? reinterpret_cast<unsigned*>(ws + L.traj) : nullptr);
+    });
+    if (rc) return rc;
+    return ln.finish();
+}
+
+int backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, float* rho_bar, int M, int N, int P, int B,
+                   int nbr, int maxit, const float* x_out, void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_multi(M, N, P, B, nbr, maxit, 0);
+    if (rc) return rc;
+    if (!x_bar || !x_out || (reinterpret_cast<uintptr_t>(x_bar) & 15) || (reinterpret_cast<uintptr_t>(x_out) & 15) ||
+        (reinterpret_cast<uintptr_t>(y_bar) & 15))
+        return fail(ADMM_E_INVALID, "x_bar, x_out (and y_bar if given) must be 16-byte aligned device pointers");
+    int flags = ADMM_MULTI_RECORD;
+    {
+        std::lock_guard<std::mutex> lk(g_rec_mu);
+        auto it = g_rec.find(workspace);
+        if (it == g_rec.end() || it->second.nbr != nbr)
+            return fail(ADMM_E_INVALID, "workspace holds no multi-branch recording of %d branches "
+                                        "(admm_tvd_forward_multi_dev_f32 with ADMM_MULTI_RECORD first)", nbr);
+        RecTag t = make_tag(M, N, P, B, 0, 0, 0, maxit, false, admm::ScalarSrc{&g_dummy_scalar, &g_dummy_scalar, 0.f, 0.f});
+        t.nbr = nbr;
+        t.masks = it->second.masks;
+        if (!(it->second == t))
+            return fail(ADMM_E_INVALID, "replay does not match its multi-branch recording (shape, maxit or library "
+                                        "options changed)");
+        if (t.masks && rho_bar)
+            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only): rho_bar cannot be "
+                                        "formed from it");
+        if (t.masks) flags |= ADMM_REC_MASKS;
+        g_rec.erase(it);
+    }
+    const size_t planes = (size_t)P * B * nbr, ppb = (size_t)P * B, MN = (size_t)M * N;
+    const MultiLayout L = make_multi_layout(planes, nbr, maxit, flags);
+    rc = check_ws(workspace, workspace_bytes, L.total);
+    if (rc) return rc;
+    unsigned char* ws = static_cast<unsigned char*>(workspace);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    Launcher ln{s, g_prof.on, {}};
+    hipError_t e;
+    const int K = maxit;
+    if (K == 0) {
+        if (y_bar && (e = hipMemsetAsync(y_bar, 0, ppb * MN * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
+        if (lambda_bar && (e = hipMemsetAsync(lambda_bar, 0, (size_t)nbr * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
+        if (rho_bar && (e = hipMemsetAsync(rho_bar, 0, (size_t)nbr * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
+        return ln.finish();
+    }
+    const admm::plane::Branches br = multi_branches(P, B, nbr);
+    const float* prm = reinterpret_cast<const float*>(ws + L.prm);
+    const bool masks = (flags & ADMM_REC_MASKS) != 0;
+    float4* dxK = rho_bar ? reinterpret_cast<float4*>(ws + L.sln) : nullptr;   // the forward's s state is dead
+    float* vbuf = y_bar ? reinterpret_cast<float*>(ws + L.hln) : nullptr;     // ... and its H^T y copies
+    double* part = reinterpret_cast<double*>(ws + L.part);
+    if (dxK) {
+        rc = ln.run(ADMM_K_PREP, [&] { return admm::plane::launch_dx_lane(x_out, dxK, planes, s, &br); });
+        if (rc) return rc;
+    }
+    rc = ln.run(ADMM_K_ADJ, [&] {
+        return admm::plane::launch_plane_adj(x_bar, ws + L.F, ws + L.traj, dxK, reinterpret_cast<float4*>(ws + L.sbar),
+                                             reinterpret_cast<float2*>(ws + L.vsl), vbuf, part,
+                                             prm, K, planes, s, &br, masks);
+    });
+    if (rc) return rc;
+    double* rt = reinterpret_cast<double*>(ws + L.rt);
+    for (int i = 0; i < nbr; ++i) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            launch_reduce_cols(s, part + 2 * (size_t)i * ppb, rt + 2 * i, (int)ppb, 2, reinterpret_cast<double*>(ws + L.rtmp));
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::grads_final_kernel, dim3(1), dim3(64), 0, s, rt + 2 * i, (const double*)nullptr,
+                               (const double*)nullptr, 0, prm + 4 * i, lambda_bar ? lambda_bar + i : nullptr,
+                               rho_bar ? rho_bar + i : nullptr, (float*)nullptr);
+        });
+        if (rc) return rc;
+    }
+    if (y_bar) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::branch_sum_kernel, dim3(1024), dim3(kThreads), 0, s, vbuf, y_bar, ppb * MN, nbr);
+        });
+        if (rc) return rc;
+    }
+    return ln.finish();
+}
+
 }  // namespace
 
 extern "C" {
@@ -1246,7 +1467,10 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
     if ((size_t)P * B > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
-    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_hbar != 0, iso != 0).total;
+    const bool want_h = (want_hbar & ADMM_REC_HBAR) != 0 && kh > 0;
+    const bool masks = (want_hbar & ADMM_REC_MASKS) != 0 && fused_shape(M, N, iso != 0) && fused_enabled() && !want_h &&
+                       fused_adj_enabled();
+    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_h, iso != 0, masks).total;
     return ADMM_OK;
 }
 
@@ -1354,6 +1578,27 @@ int admm_profile_get(int kernel_class, double* total_ms, long long* launches) {
     *total_ms = g_prof.ms[kernel_class];
     *launches = g_prof.n[kernel_class];
     return ADMM_OK;
+}
+
+int admm_tvd_multi_workspace_bytes(int M, int N, int P, int B, int nbranch, int maxit, int flags, size_t* out_bytes) {
+    if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
+    int rc = check_multi(M, N, P, B, nbranch, maxit, flags);
+    if (rc) return rc;
+    *out_bytes = make_multi_layout((size_t)P * B * nbranch, nbranch, maxit, flags).total;
+    return ADMM_OK;
+}
+
+int admm_tvd_forward_multi_dev_f32(const float* y, float* x_out, int M, int N, int P, int B, int nbranch,
+                                   const float* const* lambda, const float* const* rho, int maxit, int flags,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+    return forward_multi(y, x_out, M, N, P, B, nbranch, lambda, rho, maxit, flags, workspace, workspace_bytes, stream);
+}
+
+int admm_tvd_backward_multi_recorded_dev_f32(const float* x_bar, float* y_bar, float* lambda_bar, float* rho_bar, int M,
+                                             int N, int P, int B, int nbranch, int maxit, const float* x_out,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
+    return backward_multi(x_bar, y_bar, lambda_bar, rho_bar, M, N, P, B, nbranch, maxit, x_out, workspace,
+                          workspace_bytes, stream);
 }
 
 }  // extern "C"

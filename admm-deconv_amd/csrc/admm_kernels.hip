@@ -897,4 +897,15 @@ __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict
     pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
 }
 
+// y_bar of a multi-branch solve: out[j] = sum over the nbr branches of v[i * n + j], branch order fixed
+// (deterministic).  v: nbr consecutive blocks of n floats (each branch's input gradient).
+__global__ __launch_bounds__(kThreads) void branch_sum_kernel(const float* __restrict__ v, float* __restrict__ out,
+                                                              size_t n, int nbr) {
+    for (size_t j = (size_t)blockIdx.x * kThreads + threadIdx.x; j < n; j += (size_t)gridDim.x * kThreads) {
+        float a = v[j];
+        for (int i = 1; i < nbr; ++i) a += v[(size_t)i * n + j];
+        out[j] = a;
+    }
+}
+
 }  // namespace admm

@@ -71,7 +71,9 @@ struct BwdHead {
     size_t end;
 };
 
-inline BwdHead bwd_head(int M, int N, size_t planes, int kh, int maxit, bool want_h, bool iso) {
+// masks: the trajectory holds the fused kernel's ST mask bytes (ADMM_REC_MASKS), 32 KiB per plane and
+// iteration, instead of s_k (512 KiB)
+inline BwdHead bwd_head(int M, int N, size_t planes, int kh, int maxit, bool want_h, bool iso, bool masks = false) {
     BwdHead b{};
     b.f = make_layout(M, N, planes, kh > 0, iso);
     size_t off = b.f.total;
@@ -84,7 +86,7 @@ inline BwdHead bwd_head(int M, int N, size_t planes, int kh, int maxit, bool wan
     const int K = maxit < 1 ? 1 : maxit;
     const bool gen = generic_shape(M, N);
     const bool hq = want_h && kh > 0;
-    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * 2 * MN * 4);
+    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 8 : 2 * MN * 4));
     // forward dim-2 spectra per iteration: packed M/2 x N (power of two) or M/2+1 x N bins (generic)
     b.traj_v = hq ? take((size_t)K * planes * (gen ? (size_t)(M / 2 + 1) * N * 8 : MN * 4)) : 0;
     b.sig = hq ? take((size_t)(M / 2 + 1) * N * 16) : 0;

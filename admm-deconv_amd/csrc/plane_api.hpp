@@ -14,6 +14,18 @@ namespace admm {
 namespace plane {
 
 constexpr int kPlaneM = 256, kPlaneN = 256;
+
+// Several independent solves in one grid: the branches of a Flux Parallel(chcat, ...) that share their
+// input (the denoiser, src/nets/net_build.jl:113-125).  Grid plane q is plane q % ppb of the shared input,
+// solved with branch i = q / ppb's tables and scalars; its output goes to the chcat position of branch i
+// (image b, channel i * P + p of a (B, nbr * P, N, M) tensor).  A single solve is nbr = 1.
+struct Branches {
+    int ppb;          // planes per branch (B * P)
+    int nbr;          // branches
+    int P;            // channels per image of one branch
+    unsigned tab_f;   // floats between the branches' lane-native table blocks (tables_bytes() / 4)
+    unsigned prm_f;   // floats between the branches' {tau, rho, lambda} blocks
+};
 constexpr int kTabEntries = 2 * 32 * 512;   // lane-native spectral table entries (= 256 x 128)
 
 // bytes of the lane-native tables (Cf, C0b, Gf, G0b) carved from the workspace
@@ -28,9 +40,12 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 // [plane][n][2r + h]; s0 = x - x(line r-1), s1 = x - x(pixel p-1)); sln is then unused
 // prm: device {tau, rho, lambda} (setup_kernel); stagger: experiment option ADMM_OPT_PLANE_STAGGER (realtime
 // ticks of 10 ns that odd workgroups start late; 0 = off)
+// masks != NULL (and traj NULL): record only the ST mask bits of s_1..s_{K-1} (plane_kernel.hip mask_byte),
+// slot k-1 at masks + (k-1) * planes * 16 * 512 dwords, for a reverse sweep without rho_bar.
+// br (NULL = one solve): several branches in one grid; tables / prm then hold br->nbr consecutive blocks.
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
                         const float* prm, int K, size_t planes, hipStream_t s, float4* traj = nullptr,
-                        int stagger = 0);
+                        int stagger = 0, const Branches* br = nullptr, unsigned* masks = nullptr);
 
 
 // Reverse sweep of the anisotropic solve on the fused trajectory (plane256_adj_kernel):
@@ -38,10 +53,12 @@ hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool p
 // launch_plane_adj runs steps K..1 for every plane.  traj: the forward's s_1..s_{K-1}; sbar, vsl: planes x
 // 512 KiB / 256 KiB of state; vout: Vsum = sum_k vbar_k (natural layout; = y_bar without a PSF);
 // part: 2 doubles per plane (rho_bar, tau_bar partial sums, fixed summation order).
-hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s);
-hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
+hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s, const Branches* br = nullptr);
+// masks: traj is the mask-bit trajectory (dxK must be NULL: no rho_bar).  br: as in launch_plane (x_bar in the
+// chcat layout; vout and part per grid plane).
+hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s);
+                            hipStream_t s, const Branches* br = nullptr, bool masks = false);
 
 }  // namespace plane
 }  // namespace admm

@@ -22,6 +22,7 @@
 //   line forward  -> S
 // With a PSF the block first forms H^T y = F^-1 conj(Sigma_c) F y (ops.jl:71-81) the same way.
 #include "line_pair.hpp"
+#include "plane_api.hpp"
 
 namespace admm {
 namespace plane {
@@ -79,6 +80,39 @@ __device__ __forceinline__ void bst4(rsrc_t r, unsigned vo, unsigned so, float4 
 __device__ __forceinline__ void bst2(rsrc_t r, unsigned vo, unsigned so, float2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
 }
+__device__ __forceinline__ unsigned bldu(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+}
+__device__ __forceinline__ void bstu(rsrc_t r, unsigned vo, unsigned so, unsigned v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, vo, so, 0);
+}
+
+// Branches (plane_api.hpp): plane q of the grid is plane q % ppb of the shared input, run with branch
+// i = q / ppb's tables and scalars, its output at the chcat position of branch i (image b, channel i P + p).
+struct BranchOf {
+    int i;
+    size_t in_plane, out_plane;
+};
+__device__ __forceinline__ BranchOf branch_of(const Branches& br, size_t plane) {
+    if (br.nbr == 1) return {0, plane, plane};
+    const int i = (int)(plane / (size_t)br.ppb);
+    const size_t loc = plane - (size_t)i * br.ppb;
+    const size_t b = loc / (size_t)br.P, p = loc - b * br.P;
+    return {i, loc, (b * br.nbr + i) * br.P + p};
+}
+
+// Mask-bit trajectory (record mode 2: the reverse sweep will not form rho_bar, so it needs only the ST
+// branch of every s_k element, not s_k itself).  Per element c of a lane's register n (float4 (s1, s1', s2,
+// s2')) one byte: bits 0-3 = 1[|s_c| > tau], bits 4-7 = sign bit of s_c; 4 registers per dword, stored
+// lane-native [n / 4][t]: 32 KiB per plane and iteration instead of 512 KiB of s_k.
+__device__ __forceinline__ unsigned mask_byte(float4 s, float tau) {
+    const unsigned m = (unsigned)(fabsf(s.x) > tau) | ((unsigned)(fabsf(s.y) > tau) << 1) |
+                       ((unsigned)(fabsf(s.z) > tau) << 2) | ((unsigned)(fabsf(s.w) > tau) << 3);
+    const unsigned g = (__float_as_uint(s.x) >> 31) | ((__float_as_uint(s.y) >> 31) << 1) |
+                       ((__float_as_uint(s.z) >> 31) << 2) | ((__float_as_uint(s.w) >> 31) << 3);
+    return m | (g << 4);
+}
+constexpr unsigned kMaskSlotBytes = 16 * 512 * 4;   // one plane, one iteration
 
 // Fine-grained phase stamps (devtest timing builds only: -DPLANE_TS).
 #ifdef PLANE_TS
@@ -349,10 +383,10 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 // The chunk loop thus holds ~66 S registers instead of 128.
 // STAGED: the line inverse already parked x of registers 32..63 in the staging slots
 // (line_inverse_pair_staged); S[32..63] are dead on entry.
-template <bool STAGED = false>
+template <bool STAGED = false, bool MASK = false>
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sps, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
-                                           float tau, float rho) {
+                                           float tau, float rho, rsrc_t mrs) {
 #ifndef PLANE_CH
 #define PLANE_CH 2
 #endif
@@ -415,6 +449,7 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
     float4 wc[CH + 1];
     float2 hc[CH + 1];
     float w2x0 = 0.0f;
+    unsigned mbits = 0;   // MASK: the bytes of registers 4 (n / 4) .. n
 #pragma unroll
     for (int g = 0; g < NCH; ++g) {
         const int n0 = g * CH;
@@ -467,6 +502,13 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
 #ifndef PLANE_EXPT_NOSTORE
             bst4<PLANE_AUX_ST>(sps, t * 16, n * kPT * 16, s);
 #endif
+            if constexpr (MASK) {
+                mbits |= mask_byte(s, tau) << (8 * (n & 3));
+                if ((n & 3) == 3) {
+                    bstu(mrs, t * 4, (n >> 2) * kPT * 4, mbits);
+                    mbits = 0;
+                }
+            }
             wc[j + 1] = make_float4(phi_tau(s.x, tau), phi_tau(s.y, tau), phi_tau(s.z, tau), phi_tau(s.w, tau));
             hc[j + 1] = hyr[g % (PD + 1)][j];
             wbm[n] = make_float2(wc[j + 1].x, wc[j + 1].y);
@@ -540,12 +582,23 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
 // TRAJ: record the trajectory for the adjoint -- iteration k writes s_k to slot k-1 of `traj` (slot
 // stride traj_slot float4, lane-native layout, plane p at p * 64 * 512) and reads s_{k-1} from slot
 // k-2, instead of updating sln in place.  Same bytes per iteration as the plain solve.
-template <bool PSF, int DBG = 0, bool TRAJ = false>
+// TRAJ 2: record the ST mask bits of s_k instead (mask_byte): s stays in place in sln as in the plain solve,
+// and iteration k writes its mask slot k-1 (mtraj + (k-1) * mslot dwords, plane p at p * 16 * 512).
+// br: several branches in one grid (Branches; nbr = 1 is a single solve).
+template <bool PSF, int DBG = 0, int TRAJ = 0>
 __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__ y, float* __restrict__ x_out,
                                                        const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
                                                        float2* __restrict__ hln, float4* __restrict__ sln, const float* __restrict__ prm, int K, float2* dbg = nullptr, int stagger_ticks = 0,
-                                                       float4* __restrict__ traj = nullptr, size_t traj_slot = 0) {
+                                                       float4* __restrict__ traj = nullptr, size_t traj_slot = 0,
+                                                       Branches br = Branches{1, 1, 1, 0u, 0u},
+                                                       unsigned* __restrict__ mtraj = nullptr, size_t mslot = 0) {
+    const BranchOf bo = branch_of(br, blockIdx.x);
+    Cf += (size_t)bo.i * br.tab_f;
+    C0b += (size_t)bo.i * br.tab_f;
+    Gf = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(Gf) + (size_t)bo.i * br.tab_f);
+    G0b = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(G0b) + (size_t)bo.i * br.tab_f);
+    prm += (size_t)bo.i * br.prm_f;
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
     // late, so that the memory-heavy row phases of two groups of CUs interleave.
@@ -572,7 +625,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         sincospi((double)(q * k) / 128.0, &sn, &cs);
         tw[q * kTQ + k] = make_float2((float)cs, (float)-sn);
     }
-    const float2* yrow = reinterpret_cast<const float2*>(y + plane * 65536 + (size_t)r * 256);
+    const float2* yrow = reinterpret_cast<const float2*>(y + bo.in_plane * 65536 + (size_t)r * 256);
     float2 S[64];
 #pragma unroll
     for (int n = 0; n < 64; ++n) S[n] = yrow[2 * n + hb];
@@ -624,11 +677,17 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         }
         // iteration 1 has no s_0 to read (zero init, ops.jl:48-49): its loads go to a resource of size 0,
         // which returns zeros without touching memory
-        if constexpr (TRAJ) {
+        if constexpr (TRAJ == 1) {
             float4* tb = traj + plane * 64 * kPT;
             const rsrc_t sld = make_rsrc(tb + (size_t)(k >= 2 ? k - 2 : 0) * traj_slot, k >= 2 ? 64 * kPT * 16 : 0);
             const rsrc_t sst = make_rsrc(tb + (size_t)(k - 1) * traj_slot, 64 * kPT * 16);
-            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho, sld);
+        } else if constexpr (TRAJ == 2) {
+            // s in place as below (s_{K-1} is not stored: only its mask bits are needed after the solve)
+            const rsrc_t sld = k >= 2 ? sp : make_rsrc(sln, 0);
+            const rsrc_t sst = k <= K - 2 ? sp : make_rsrc(sln, 0);
+            const rsrc_t mrs = make_rsrc(mtraj + (size_t)(k - 1) * mslot + plane * 16 * kPT, kMaskSlotBytes);
+            row_update<kStage, true>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho, mrs);
         } else {
             // ... and s_{K-1} is never read (iteration K stops at x): its stores drop the same way
             const rsrc_t sld = k >= 2 ? sp : make_rsrc(sln, 0);
@@ -637,14 +696,14 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
 #pragma unroll
                 for (int m = 0; m < 32; ++m) S[32 + m] = colbuf[t + m * kPT];
             } else {
-                row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho);
+                row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho, sld);
             }
         }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
         if constexpr (!(PLANE_EXPT_SKIP & 2)) line_forward_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k, t);
     }
-    float2* xrow = reinterpret_cast<float2*>(x_out + plane * 65536 + (size_t)r * 256);
+    float2* xrow = reinterpret_cast<float2*>(x_out + bo.out_plane * 65536 + (size_t)r * 256);
 #pragma unroll
     for (int n = 0; n < 64; ++n) xrow[2 * n + hb] = S[n];
 }
@@ -674,6 +733,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
 #ifndef ADJX
 #define ADJX 0
 #endif
+template <bool MASK>
 __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t s2p, rsrc_t sbl, rsrc_t sbs, rsrc_t vlp,
                                             rsrc_t vsp, unsigned vso, unsigned vss, float2* xb, float2* wb,
                                             float2* sink, float2* colbuf, int t, bool hb, bool lastk, float tau,
@@ -682,6 +742,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
     const bool top = lane < 2, bot = lane >= 62;
     float4 s1r[2], s2r[2], sbr[2];
     float2 vr[2];
+    unsigned mwr[2];   // MASK: s1p is the mask-bit slot of s_{k-1} (one dword per 4 registers)
     float2* stg = colbuf + t;
     float2* stg2 = stg + 16 * kPT;
     if (bot) {
@@ -695,8 +756,12 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
     const float v63y = stg2[15 * kPT].y;
     lds_barrier();
     sched_fence();
-    s1r[0] = bld4(s1p, t * 16, 0);
-    s2r[0] = bld4(s2p, t * 16, 0);
+    if constexpr (MASK) {
+        mwr[0] = bldu(s1p, t * 4, 0);
+    } else {
+        s1r[0] = bld4(s1p, t * 16, 0);
+        s2r[0] = bld4(s2p, t * 16, 0);
+    }
     sbr[0] = bld4(sbl, t * 16, 0);
     vr[0] = bld2(vlp, t * 8, 0);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
@@ -708,12 +773,16 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
     for (int n = 0; n < 64; ++n) {
         if (n + 1 < 64) {
             const int q = (n + 1) & 1;
-            __asm__ volatile("" ::"v"(s1r[q].x), "v"(s1r[q].y), "v"(s1r[q].z), "v"(s1r[q].w), "v"(s2r[q].x),
-                             "v"(s2r[q].y), "v"(s2r[q].z), "v"(s2r[q].w));
+            if constexpr (MASK) {
+                if (((n + 1) & 3) == 0) mwr[((n + 1) >> 2) & 1] = bldu(s1p, t * 4, ((n + 1) >> 2) * kPT * 4);
+            } else {
+                __asm__ volatile("" ::"v"(s1r[q].x), "v"(s1r[q].y), "v"(s1r[q].z), "v"(s1r[q].w), "v"(s2r[q].x),
+                                 "v"(s2r[q].y), "v"(s2r[q].z), "v"(s2r[q].w));
+            }
             __asm__ volatile("" ::"v"(sbr[q].x), "v"(sbr[q].y), "v"(sbr[q].z), "v"(sbr[q].w), "v"(vr[q].x),
                              "v"(vr[q].y));
-            if (!(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + 1) * kPT * 16);
-            if (!(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + 1) * kPT * 16);
+            if (!MASK && !(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + 1) * kPT * 16);
+            if (!MASK && !(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + 1) * kPT * 16);
             if (!(ADJX & 4)) sbr[q] = bld4(sbl, t * 16, (n + 1) * kPT * 16);
             if (!(ADJX & 2)) vr[q] = bld2(vlp, t * 8, (n + 1) * kPT * 8);
         }
@@ -733,7 +802,9 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
             S[63] = stg2[15 * kPT];
             sched_fence();
         }
-        const float4 s1 = s1r[n & 1], s2 = s2r[n & 1], sb = sbr[n & 1];
+        const float4 s1 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s1r[n & 1];
+        const float4 s2 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s2r[n & 1];
+        const float4 sb = sbr[n & 1];
         const float2 vo = vr[n & 1];
         const float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
@@ -745,6 +816,21 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         const float a1[4] = {s1.x, s1.y, s1.z, s1.w}, a2[4] = {s2.x, s2.y, s2.z, s2.w};
         const float b[4] = {sb.x, sb.y, sb.z, sb.w};
         float nb[4];
+        if constexpr (MASK) {
+            // rho_bar is not formed in this mode (its <D vbar, D x_k> needs s_k itself): only the branch
+            // decisions enter -- bitwise the same sbar and tau_bar as from the full trajectory
+            const unsigned byte = mwr[(n >> 2) & 1] >> (8 * (n & 3));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float wbv = rho * dv[c];
+                const bool m = (byte >> c) & 1u;
+                nb[c] = m ? wbv : b[c] - wbv;
+                const float sg = ((byte >> (4 + c)) & 1u) ? -1.0f : 1.0f;
+                tacc += m ? sg * (b[c] - 2.0f * wbv) : 0.0f;
+            }
+            (void)a1;
+            (void)a2;
+        } else {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const float dx = lastk ? a2[c] : a2[c] - clip_tau(a1[c], tau);
@@ -755,6 +841,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
             racc += phi_tau(a1[c], tau) * dv[c];
             const float sg = (a1[c] > 0.f) ? 1.0f : -1.0f;
             tacc += m ? sg * (b[c] - 2.0f * wbv) : 0.0f;
+        }
         }
         // pin the accumulators here: left free, the compiler sinks the sums to the end of the
         // unrolled loop and keeps every register's operands live until then (~2000 VGPRs of spills)
@@ -790,11 +877,13 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
 
 // D x_K in the lane-native s layout (entry [n][t] = (d0[p], d0[p+1], d1[p], d1[p+1]) of pixel pair
 // p = 4n + 2h of line r, t = 2r + h): the reverse sweep's step-K operand.  grid (128, planes) x 256.
-__global__ __launch_bounds__(256) void dx_lane_kernel(const float* __restrict__ x, float4* __restrict__ out) {
+// br: x_K in the chcat layout of several branches (grid plane q reads output plane branch_of(q).out_plane).
+__global__ __launch_bounds__(256) void dx_lane_kernel(const float* __restrict__ x, float4* __restrict__ out,
+                                                      Branches br) {
     const int idx = blockIdx.x * 256 + threadIdx.x;   // [n][t]
     const int n = idx >> 9, t = idx & 511;
     const int r = t >> 1, p = 4 * n + 2 * (t & 1);
-    const float* xp = x + (size_t)blockIdx.y * 65536;
+    const float* xp = x + branch_of(br, blockIdx.y).out_plane * 65536;
     const float2 c = *reinterpret_cast<const float2*>(xp + r * 256 + p);
     const float2 u = *reinterpret_cast<const float2*>(xp + ((r + 255) & 255) * 256 + p);
     const float l = xp[r * 256 + ((p + 255) & 255)];
@@ -806,12 +895,20 @@ __global__ __launch_bounds__(256) void dx_lane_kernel(const float* __restrict__ 
 //   dxK     : D x_K (dx_lane_kernel)                           sbar : lane-native sbar state (in place)
 //   vsl     : lane-native Vsum accumulator                     vout : Vsum = sum_k vbar_k, natural layout
 //   part    : per plane (rho_bar partial, tau_bar partial) in fp64
+//   MASK    : traj is the mask-bit trajectory (plane256_kernel TRAJ 2; traj_slot in dwords); no dxK
+//   br      : several branches in one grid (x_bar in the chcat layout; vout, part per grid plane)
+template <bool MASK>
 __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restrict__ xbar, const float* __restrict__ Cf,
                                                            const float* __restrict__ C0b,
-                                                           const float4* __restrict__ traj, size_t traj_slot,
+                                                           const void* __restrict__ traj, size_t traj_slot,
                                                            const float4* __restrict__ dxK, float4* __restrict__ sbar,
                                                            float2* __restrict__ vsl, float* __restrict__ vout,
-                                                           double* __restrict__ part, const float* __restrict__ prm, int K) {
+                                                           double* __restrict__ part, const float* __restrict__ prm, int K,
+                                                           Branches br) {
+    const BranchOf bo = branch_of(br, blockIdx.x);
+    Cf += (size_t)bo.i * br.tab_f;
+    C0b += (size_t)bo.i * br.tab_f;
+    prm += (size_t)bo.i * br.prm_f;
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* colbuf = reinterpret_cast<float2*>(smem_raw);
@@ -832,14 +929,15 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         sincospi((double)(q * k) / 128.0, &sn, &cs);
         tw[q * kTQ + k] = make_float2((float)cs, (float)-sn);
     }
-    const float2* grow = reinterpret_cast<const float2*>(xbar + plane * 65536 + (size_t)r * 256);
+    const float2* grow = reinterpret_cast<const float2*>(xbar + bo.out_plane * 65536 + (size_t)r * 256);
     float2 S[64];
 #pragma unroll
     for (int n = 0; n < 64; ++n) S[n] = grow[2 * n + hb];
     const rsrc_t cfr = make_rsrc(Cf, kTab * 4);
     const rsrc_t none = make_rsrc(Cf, 0);
     constexpr unsigned kS4 = 64 * kPT * 16, kS2 = 64 * kPT * 8;
-    const float4* tb = traj + plane * 64 * kPT;
+    const float4* tb = static_cast<const float4*>(traj) + plane * 64 * kPT;
+    const unsigned* mb = static_cast<const unsigned*>(traj) + plane * 16 * kPT;
     float4* sbp = sbar + plane * 64 * kPT;
     float2* vlp = vsl + plane * 64 * kPT;
     double rsum = 0.0, tsum = 0.0;
@@ -848,7 +946,9 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         column_half<0, 0>(S, colbuf, tw, mir, cfr, c0l, none, nullptr, t, hb);
         column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, none, nullptr, t, hb);
         line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
-        const rsrc_t s1p = k >= 2 ? make_rsrc(tb + (size_t)(k - 2) * traj_slot, kS4) : none;
+        const rsrc_t s1p = k < 2 ? none
+                           : MASK ? make_rsrc(mb + (size_t)(k - 2) * traj_slot, kMaskSlotBytes)
+                                  : make_rsrc(tb + (size_t)(k - 2) * traj_slot, kS4);
         // s_k / D x_K feed only rho_bar's <D vbar, D x_k>: without dxK (rho_bar not wanted) they read as 0
         const rsrc_t s2p = !dxK ? none : k == K ? make_rsrc(dxK + plane * 64 * kPT, kS4) : make_rsrc(tb + (size_t)(k - 1) * traj_slot, kS4);
         const rsrc_t sbl = k < K ? make_rsrc(sbp, kS4) : none;
@@ -863,7 +963,7 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         const unsigned vss = k >= 2 ? kPT * 8 : 16;
         float racc = 0.0f, tacc = 0.0f;
 #if !(ADJX & 1)
-        row_adjoint(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
+        row_adjoint<MASK>(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
                     tacc);
 #endif
         rsum += racc;

@@ -30,43 +30,59 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
     return hipGetLastError();
 }
 
-template <bool PSF, bool TRAJ>
+static Branches one_branch() { return Branches{1, 1, 1, 0u, 0u}; }
+
+template <bool PSF, int TRAJ>
 static void launch_one(const float* y, float* x_out, const Tables& t, float2* hln, float4* sln, const float* prm,
-                       int K, size_t planes, hipStream_t s, int stagger, float4* traj) {
+                       int K, size_t planes, hipStream_t s, int stagger, float4* traj, const Branches& br,
+                       unsigned* masks) {
     (void)hipFuncSetAttribute((const void*)plane256_kernel<PSF, 0, TRAJ>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kLdsBytes);
     hipLaunchKernelGGL((plane256_kernel<PSF, 0, TRAJ>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out,
                        t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, prm, K, nullptr, stagger, traj,
-                       planes * 64 * kPT);
+                       planes * 64 * kPT, br, masks, planes * 16 * kPT);
 }
 
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj, int stagger) {
+                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj, int stagger,
+                        const Branches* brp, unsigned* masks) {
     const Tables t = carve(tables);
-    if (psf) {
-        if (traj) launch_one<true, true>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
-        else launch_one<true, false>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
-    } else {
-        if (traj) launch_one<false, true>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
-        else launch_one<false, false>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj);
+    const Branches br = brp ? *brp : one_branch();
+    const int mode = traj ? 1 : masks ? 2 : 0;
+#define X(P, M)                                                                                     \
+    if (psf == P && mode == M) {                                                                    \
+        launch_one<P, M>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj, br, masks);       \
+        return hipGetLastError();                                                                   \
     }
-    return hipGetLastError();
+    X(false, 0) X(false, 1) X(false, 2) X(true, 0) X(true, 1) X(true, 2)
+#undef X
+    return hipErrorInvalidValue;
 }
 
 
-hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s) {
-    hipLaunchKernelGGL(dx_lane_kernel, dim3(64 * kPT / 256, (unsigned)planes), dim3(256), 0, s, xK, dxK);
+hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream_t s, const Branches* brp) {
+    hipLaunchKernelGGL(dx_lane_kernel, dim3(64 * kPT / 256, (unsigned)planes), dim3(256), 0, s, xK, dxK,
+                       brp ? *brp : one_branch());
     return hipGetLastError();
 }
 
-hipError_t launch_plane_adj(const float* xbar, const void* tables, const float4* traj, const float4* dxK, float4* sbar,
+hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s) {
+                            hipStream_t s, const Branches* brp, bool masks) {
     const Tables t = carve(tables);
-    (void)hipFuncSetAttribute((const void*)plane256_adj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kLdsBytes);
-    hipLaunchKernelGGL(plane256_adj_kernel, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf, t.C0b, traj,
-                       planes * 64 * kPT, dxK, sbar, vsl, vout, part, prm, K);
+    const Branches br = brp ? *brp : one_branch();
+    if (masks) {
+        if (dxK) return hipErrorInvalidValue;   // rho_bar needs the full trajectory
+        (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_adj_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
+                           t.C0b, traj, planes * 16 * kPT, dxK, sbar, vsl, vout, part, prm, K, br);
+    } else {
+        (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_adj_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
+                           t.C0b, traj, planes * 64 * kPT, dxK, sbar, vsl, vout, part, prm, K, br);
+    }
     return hipGetLastError();
 }
 

@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--distinct", type=int, default=64, help="distinct synthetic images generated per rank (tiled)")
     ap.add_argument("--serial-branches", action="store_true",
                     help="c5: run the Parallel branches one after the other on one stream (the reference's order)")
+    ap.add_argument("--no-merge", action="store_true",
+                    help="c5: solve the Parallel branches one by one (per-branch streams) instead of one grid")
     ap.add_argument("--iso", action="store_true",
                     help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
     return ap.parse_args()
@@ -127,7 +129,9 @@ def bench_c5(args, dev):
     x = torch.from_numpy(np.concatenate([noisy] * reps)[:B]).to(dev)
     target = torch.from_numpy(np.concatenate([clean] * reps)[:B]).to(dev).repeat(1, len(branch), 1, 1)
 
-    net = layers.Parallel(layers.chcat, *branch, streams=not args.serial_branches)   # net_build.jl:121-125
+    net = layers.Parallel(layers.chcat, *branch, streams=not args.serial_branches,   # net_build.jl:121-125
+                          merge=not (args.no_merge or args.serial_branches))
+    merged = net._mergeable(x)
 
     def step():
         out = net(x)                                          # 5 branches on their own HIP streams, chcat
@@ -161,12 +165,34 @@ def bench_c5(args, dev):
         if n:
             kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
     roof = None
-    if not args.iso and kernels.get("adjoint", {}).get("launches_per_step") == len(branch):
+    planes = B * P
+    if merged:
+        # one grid of 5 x 192 planes for the forward (plane256_kernel recording ST mask bits: lambda is the
+        # only trainable, rho_bar is not formed) and one for the reverse sweep (plane256_adj_kernel<masks>).
+        # Per pixel: forward y in, H^T y copy out (4 + 4), per iteration H^T y in (4, K-1 times), s in / out
+        # (8 + 8, K-2 times), mask byte per pixel pair out (0.5, K-1 times), x out (4);
+        # reverse: x_bar in (4), per step sbar in, sbar out (8 + 8), mask in (0.5), K-1 times each
+        nb = len(branch)
+        fwd_px = 12 + 4 * (K - 1) + 16 * (K - 2) + 0.5 * (K - 1)
+        adj_px = 4 + 16.5 * (K - 1)
+        per = {"plane": nb * planes * M * N * fwd_px, "adjoint": nb * planes * M * N * adj_px}
+        for k, b in per.items():
+            if k in kernels:
+                kernels[k]["algorithmic_bytes_per_launch"] = b
+                kernels[k]["achieved_GBps"] = round(b / (kernels[k]["avg_ms"] * 1e-3) / 1e9, 1)
+        dom = max((k for k in per if k in kernels), key=lambda k: kernels[k]["total_ms_per_step"])
+        a = kernels[dom]
+        ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": f"{dom} (one grid of {nb} branches x {planes} planes)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic("c5m", dom), "algorithmic_bytes_per_launch": per[dom],
+                "avg_launch_ms": round(a["avg_ms"], 5)}
+    elif not args.iso and kernels.get("adjoint", {}).get("launches_per_step") == len(branch):
         # fused reverse sweep (plane256_adj_kernel, one launch per layer).  The input and rho need no gradient,
-        # so the sweep gets neither y_bar nor rho_bar and reads no Vsum and no s_k; per pixel: s_{k-1},
-        # sbar_k in, sbar_{k-1} out (K-1 steps each, 8 B) and x_bar in (4 B): (24 K - 20) B/px
-        planes = B * P
-        per_launch = planes * M * N * (24 * K - 20)
+        # so the sweep gets neither y_bar nor rho_bar and reads no Vsum and no s_k; per pixel: the ST mask
+        # byte of s_{k-1} (one byte per lane pixel pair: 0.5 B/px), sbar_k in, sbar_{k-1} out (K-1 steps each, 8 B)
+        # and x_bar in (4 B): 4 + 16.5 (K - 1) B/px
+        per_launch = planes * M * N * (4 + 16.5 * (K - 1))
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "adjoint (plane256_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -175,7 +201,6 @@ def bench_c5(args, dev):
     elif not args.iso and "adjoint" in kernels:
         # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1},
         # sbar_k, sbar_{k-1} (8 M N each; no s_k and no Vsum: neither rho_bar nor y_bar requested)
-        planes = B * P
         per_launch = planes * (16 * (M // 2) * N + 24 * M * N)
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
@@ -189,7 +214,8 @@ def bench_c5(args, dev):
         "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
                                "GMSD loss (HIP), backward through the recorded adjoint "
-                               f"({'iso' if args.iso else 'aniso'})", "global_batch": B},
+                               f"({'iso' if args.iso else 'aniso'}; "
+                               f"{'branches in one grid' if merged else 'per-branch solves'})", "global_batch": B},
         "roofline": roof, "kernels": kernels}))
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define ADMM_ABI_VERSION 2
+#define ADMM_ABI_VERSION 3
 
 enum {
     ADMM_OK = 0,
@@ -54,7 +54,7 @@ enum {
     ADMM_K_FINAL = 4,   /* last irFFT along dim1, writes x                                       */
     ADMM_K_NORM = 5,    /* isotropic only: pixelnorm over the batch (ops.jl:6)                   */
     ADMM_K_PLANE = 6,   /* fused per-plane solve, all K iterations (256 x 256, anisotropic)      */
-    ADMM_K_ADJ = 7,     /* adjoint reverse-step line kernels (line_adj, iso_adj_a / iso_adj_b)   */
+    ADMM_K_ADJ = 7,     /* adjoint reverse-step kernels (line_adj, iso_adj_a / iso_adj_b, fused)  */
     ADMM_K_COUNT = 8
 };
 
@@ -142,6 +142,17 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
  * that differs (or a workspace that holds no recording -- a plain forward on it overwrites one)
  * fails with ADMM_E_INVALID rather than reading a trajectory of another layout.  A recording is
  * consumed by its replay. */
+/* `want_hbar` of the record entry points (and of admm_tvd_backward_workspace_bytes) is a flag word:
+ *   ADMM_REC_HBAR  (1): also record what h_bar needs (the replay must then be given h_bar);
+ *   ADMM_REC_MASKS (2): the replay will not be asked for rho_bar -- record only the soft-threshold
+ *       branch of every trajectory element (1[|s_k| > tau] and sign(s_k), 1 byte per pixel pair and
+ *       iteration) instead of s_k itself: 16x less trajectory memory and, in the fused
+ *       256 x 256 anisotropic reverse sweep, 8 of its 24 B/px per step gone.  lambda_bar, y_bar and h_bar
+ *       are bitwise those of a full recording; a replay with rho_bar != NULL fails with ADMM_E_INVALID.
+ *       Honoured by the fused anisotropic trajectory (256 x 256, no h_bar); elsewhere the full
+ *       trajectory is recorded and rho_bar stays available. */
+enum { ADMM_REC_HBAR = 1, ADMM_REC_MASKS = 2 };
+
 int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B,
                                 const float* h, int kh, int kw, float lambda, float rho, int iso,
                                 int maxit, int want_hbar, void* workspace, size_t workspace_bytes,
@@ -180,6 +191,32 @@ int admm_tvd_backward_recorded_dev_f32(const float* y, const float* x_bar, float
                                        const float* lambda, const float* rho, int iso, int maxit,
                                        const float* x_out, void* workspace, size_t workspace_bytes,
                                        void* stream, const admm_batch_reducer* reducer);
+
+/* Several solves of ONE shared input in one launch: the branches of a Flux
+ * `Parallel(chcat, b_1, ..., b_nbranch)` whose branches are ADMM layers without a PSF (the denoiser,
+ * src/nets/net_build.jl:113-125: five ADMMDeconvF2((), 50, ρ_i, relu1)).  Branch i solves every plane
+ * of y with its own λ_i, ρ_i (device pointers: lambda[i], rho[i] -- host arrays of `nbranch` device
+ * pointers) and writes the chcat layout: x_out is Julia (M, N, nbranch*P, B) == C
+ * `float[B][nbranch*P][N][M]`, branch i's channels at i*P .. i*P+P-1 -- the output of
+ * `Parallel(chcat, ...)` itself, before the layers' bias / σ.  All nbranch*P*B planes run in one grid of
+ * the fused kernel, so no CU idles between branches.  Anisotropic, 256 x 256, no PSF, at most 65,280
+ * planes in total (nbranch*P*B); the same results, bitwise, as nbranch separate solves.
+ * flags: ADMM_MULTI_RECORD (1) records the trajectory for admm_tvd_backward_multi_recorded_dev_f32
+ *        (the workspace then holds it until the replay); | ADMM_REC_MASKS (2) as above (no rho_bar).
+ * The backward writes lambda_bar[i] (and rho_bar[i]; device arrays of nbranch floats, NULL = not
+ * needed; rho_bar must be NULL with ADMM_REC_MASKS) and y_bar = the sum over branches of each branch's
+ * input gradient (NULL = not needed, cheaper), from x_bar in the chcat layout of x_out.  x_out must
+ * still hold the recorded output. */
+enum { ADMM_MULTI_RECORD = 1 };
+int admm_tvd_multi_workspace_bytes(int M, int N, int P, int B, int nbranch, int maxit, int flags,
+                                   size_t* out_bytes);
+int admm_tvd_forward_multi_dev_f32(const float* y, float* x_out, int M, int N, int P, int B, int nbranch,
+                                   const float* const* lambda, const float* const* rho, int maxit, int flags,
+                                   void* workspace, size_t workspace_bytes, void* stream);
+int admm_tvd_backward_multi_recorded_dev_f32(const float* x_bar, float* y_bar, float* lambda_bar,
+                                             float* rho_bar, int M, int N, int P, int B, int nbranch,
+                                             int maxit, const float* x_out, void* workspace,
+                                             size_t workspace_bytes, void* stream);
 
 /* Library options: process-global switches read at each call.  The defaults are the tuned choices;
  * the others exist for tests (fused vs 2-pass paths) and tuning experiments.  Not read from the

@@ -42,7 +42,7 @@ def _make_C(M, N, rho, h):
     return 1.0 / (s2 + rho * lap)
 
 
-def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, record=None):
+def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, record=None, tau=None, terms=None):
     """y: (B,P,N,M) float64 tensor; lam, rho: 0-d tensors; h: (kw,kh) tensor or None.  Returns x.
 
     masks (optional): the prox's branch decisions held fixed, one entry per iteration k = 1..maxit-1 --
@@ -53,9 +53,25 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
     same way (Zygote / autograd differentiate the selected branch).  Used to condition the gradient
     oracle on the ST / BT masks of an fp32 implementation's own forward (tests/test_gpu_adjoint_masked.py):
     fp32 and fp64 forwards flip different mask bits where |s_k| is within rounding of tau.
-    record (optional list): receives (s_k as (B,P,2,N,M), ||s_k|| as (N,M)) for k = 1..maxit-1."""
+    record (optional list): receives (s_k as (B,P,2,N,M), ||s_k|| as (N,M)) for k = 1..maxit-1.
+    tau (optional): the threshold as its own variable (default lam / rho, ops.jl:20) -- splits rho's
+    gradient into its explicit part and the part through tau (tvd_fft_grads_split).
+    terms (optional dict): every use of rho and tau gets its own elementwise copy (lists terms["rho"],
+    terms["tau"]; retain_grad), so that after backward() the sum of |grad| over them is the sum of the
+    absolute values of the terms rho_bar and tau_bar add up -- the scale fp summation error is measured
+    against (the gradients are heavily cancelling sums)."""
     B, P, N, M = y.shape
-    tau = lam / rho                                                   # ops.jl:20
+    if tau is None:
+        tau = lam / rho                                               # ops.jl:20
+    rho0, tau0 = rho, tau
+
+    def _own(v, shape, kind):
+        if terms is None:
+            return v
+        c = v.expand(shape).clone()
+        c.retain_grad()
+        terms.setdefault(kind, []).append(c)
+        return c
     C = _make_C(M, N, rho, h)
     hty = y if h is None else _ht(y, h)
     x = torch.zeros_like(y)
@@ -64,6 +80,9 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
     for it in range(maxit):
         w1, w2 = z1 - u1, z2 - u2
         dtw = (w1 - torch.roll(w1, -1, dims=-2)) + (w2 - torch.roll(w2, -1, dims=-1))
+        if terms is not None:
+            C = _make_C(M, N, _own(rho0, (N, M // 2 + 1), "rho"), h)
+            rho = _own(rho0, y.shape, "rho")
         x = torch.fft.irfft2(C * torch.fft.rfft2(hty + rho * dtw), s=(N, M))
         d1 = x - torch.roll(x, 1, dims=-2)                             # x[i,j]-x[i,j-1]
         d2 = x - torch.roll(x, 1, dims=-1)                             # x[i,j]-x[i-1,j]
@@ -72,6 +91,11 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
             record.append((torch.stack([s1, s2], dim=2).detach(),
                            torch.sqrt((s1 * s1 + s2 * s2).sum(dim=(0, 1))).detach()))
         fixed = masks is not None and it < len(masks)
+        if terms is not None and it < maxit - 1:   # (the last iteration's prox output is dead)
+            tau = _own(tau0, (1, 1, N, M) if isotropic else y.shape, "tau")
+            tau_b = tau if isotropic else _own(tau0, y.shape, "tau")
+        else:
+            tau_b = tau
         if isotropic:
             nrm = torch.sqrt((s1 * s1 + s2 * s2).sum(dim=(0, 1), keepdim=True))
             if fixed:
@@ -83,10 +107,10 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
         elif fixed:
             m, sg = (torch.as_tensor(a, dtype=y.dtype) for a in masks[it])
             z1 = m[:, :, 0] * (s1 - sg[:, :, 0] * tau)
-            z2 = m[:, :, 1] * (s2 - sg[:, :, 1] * tau)
+            z2 = m[:, :, 1] * (s2 - sg[:, :, 1] * tau_b)
         else:
             z1 = torch.sign(s1) * torch.clamp(torch.abs(s1) - tau, min=0.0)
-            z2 = torch.sign(s2) * torch.clamp(torch.abs(s2) - tau, min=0.0)
+            z2 = torch.sign(s2) * torch.clamp(torch.abs(s2) - tau_b, min=0.0)
         u1, u2 = u1 + d1 - z1, u2 + d2 - z2
     return x
 
@@ -116,3 +140,25 @@ def masks_from_trajectory(s_traj, lam, rho, iso, nrm_traj=None):
     if iso:
         return [(np.asarray(n) > tau).astype(np.float64) for n in nrm_traj]
     return [((np.abs(s) > tau).astype(np.float64), np.sign(s).astype(np.float64)) for s in s_traj]
+
+
+def tvd_fft_grads_split(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64, masks=None, scales=None):
+    """Gradients with tau = lam / rho as its own variable: returns (x, ybar, hbar, tau_bar, rho_bar_explicit).
+    Then lam_bar = tau_bar / rho and rho_bar = rho_bar_explicit - tau_bar lam / rho^2.
+    scales (optional dict): receives "tau" = sum of |terms| of tau_bar and "rho" = of rho_bar_explicit (see
+    tvd_fft_torch `terms`): the condition scales of the two cancelling sums."""
+    y = torch.as_tensor(y, dtype=dtype).clone().requires_grad_(True)
+    lam_v = float(lam)
+    rho_t = torch.tensor(float(rho), dtype=dtype, requires_grad=True)
+    tau_t = torch.tensor(float(lam) / float(rho), dtype=dtype, requires_grad=True)
+    h_t = None
+    if h is not None and h.size:
+        h_t = torch.as_tensor(h, dtype=dtype).clone().requires_grad_(True)
+    terms = {} if scales is not None else None
+    x = tvd_fft_torch(y, torch.tensor(lam_v, dtype=dtype), rho_t, h_t, iso, maxit, masks, tau=tau_t, terms=terms)
+    (x * torch.as_tensor(xbar, dtype=dtype)).sum().backward()
+    if scales is not None:
+        for k in ("tau", "rho"):
+            scales[k] = float(sum(t.grad.abs().sum() for t in terms.get(k, []) if t.grad is not None))
+    g = lambda t: float(t.grad) if t.grad is not None else 0.0  # noqa: E731
+    return (x.detach().numpy(), y.grad.numpy(), None if h_t is None else h_t.grad.numpy(), g(tau_t), g(rho_t))

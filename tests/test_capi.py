@@ -29,7 +29,7 @@ def test_library_exports_every_symbol():
     L = _lib.load()
     for name in header_functions():
         assert hasattr(L, name), name
-    assert L.admm_abi_version() == 2
+    assert L.admm_abi_version() == 3
 
 
 def test_workspace_bytes():
@@ -166,3 +166,22 @@ def test_backward_y_bar_optional_but_aligned():
                                  fake, fake, 1 << 30, None)
     assert rc == _lib.ADMM_E_INVALID
     assert b"y_bar" in L.admm_last_error()
+
+
+def test_multi_branch_workspace_and_validation():
+    """admm_tvd_multi_workspace_bytes: the one-grid multi-branch solve covers 256 x 256 only, checks its
+    flags, and a recording with ADMM_REC_MASKS needs far less trajectory memory than a full one."""
+    L = _lib.load()
+    out = ctypes.c_size_t(0)
+    assert L.admm_tvd_multi_workspace_bytes(128, 128, 3, 2, 5, 10, 0, ctypes.byref(out)) == _lib.ADMM_E_UNSUPPORTED
+    assert L.admm_tvd_multi_workspace_bytes(256, 256, 3, 2, 5, 10, 8, ctypes.byref(out)) == _lib.ADMM_E_INVALID
+    assert L.admm_tvd_multi_workspace_bytes(256, 256, 3, 2, 0, 10, 0, ctypes.byref(out)) == _lib.ADMM_E_INVALID
+    plain = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, 0)
+    full = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_RECORD)
+    masks = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_RECORD | _lib.REC_MASKS)
+    planes, px = 5 * 3 * 64, 256 * 256
+    assert full - plain >= 49 * planes * px * 8 and masks - plain < 49 * planes * px * 8 / 8
+    # the single-solve recording with ADMM_REC_MASKS is sized for the mask trajectory too
+    f = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, 0)
+    m = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, _lib.REC_MASKS)
+    assert m < f

@@ -99,10 +99,33 @@ def test_parallel_no_grad_streams_match_serial(dev):
     br = [layers.ADMMDeconvF2((), 12, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.02, 0.2, 2.0)]
     x, _ = _inputs(dev, 4, 256, 256, 0, P=3, g0=40)
     with torch.no_grad():
-        par = layers.Parallel(layers.chcat, *br, streams=True)(x)
-        ser = layers.Parallel(layers.chcat, *br, streams=False)(x)
+        par = layers.Parallel(layers.chcat, *br, streams=True, merge=False)(x)
+        ser = layers.Parallel(layers.chcat, *br, streams=False, merge=False)(x)
+        mer = layers.Parallel(layers.chcat, *br)(x)   # one grid for all branches (ops.tvd_fft_multi)
     torch.cuda.synchronize()
     assert torch.equal(par, ser)
+    assert torch.equal(mer, ser)
+
+
+def test_merged_parallel_step_never_syncs_the_host(dev):
+    """The one-grid Parallel(chcat) of the c5 denoiser (net_build.jl:113-128), forward + backward, under
+    torch's sync-debug mode (raises on any device-to-host read)."""
+    rng = np.random.default_rng(4)
+    br = [layers.ADMMDeconvF2((), 6, r, layers.relu1, rng=rng, device=dev) for r in (0.02, 0.2, 2.0)]
+    for L in br:
+        L.lam.requires_grad_(True)
+    net = layers.Parallel(layers.chcat, *br)
+    y3, _ = _inputs(dev, 2, 256, 256, 0, P=3)
+    assert net._mergeable(y3)
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        out = net(y3)
+        out.square().sum().backward()
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    assert all(L.lam.grad is not None for L in br) and torch.isfinite(out).all()
 
 
 def test_replay_rejects_changed_options(dev):

@@ -66,27 +66,37 @@ def test_creg_clamp(dev):
     assert abs(L.lam.item() - 0.01) < 1e-7 and abs(L.rho.item() - 0.01) < 1e-7
 
 
-def test_parallel_branches_on_streams_match_serial(dev):
-    """Parallel(chcat, ...) (net_build.jl:121-125) with every branch on its own HIP stream gives the same
-    forward output and the same parameter / input gradients, bitwise, as the branches run serially."""
+@pytest.mark.parametrize("train_rho", [False, True], ids=["lam", "lam+rho"])
+def test_parallel_branches_on_streams_match_serial(dev, train_rho):
+    """Parallel(chcat, ...) (net_build.jl:121-125): the branches in ONE grid (the default for ADMM branches
+    the fused kernel covers), each branch on its own HIP stream, and the branches run one after the other
+    give the same forward output and the same parameter gradients, bitwise; the input gradient (a sum over
+    the branches, added in a different order) to fp32 rounding.  train_rho: rho trainable too, so the
+    recordings keep the full trajectory instead of the ST mask bits."""
     from admm_deconv import layers
     x0 = torch.from_numpy(synth.make_batch(3, 256, 256, None, P=3, sigma=0.1)).to(dev)
     grads = []
-    for streams in (True, False):
+    for streams, merge in ((True, False), (False, False), (True, True)):
         rng = np.random.default_rng(5)
         branch = [layers.ADMMDeconvF2((), 12, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.2, 4.0)]
         for L in branch:
             L.lam.requires_grad_(True)
-        net = layers.Parallel(layers.chcat, *branch, streams=streams)
+            L.rho.requires_grad_(train_rho)
+        net = layers.Parallel(layers.chcat, *branch, streams=streams, merge=merge)
+        assert net._mergeable(x0) == merge
         x = x0.clone().requires_grad_(True)
         out = net(x)
         (out * torch.linspace(0, 1, out.shape[1], device=dev).reshape(1, -1, 1, 1)).sum().backward()
         torch.cuda.synchronize()
-        grads.append((out.detach(), x.grad, [L.lam.grad for L in branch]))
-    (o1, g1, l1), (o2, g2, l2) = grads
+        grads.append((out.detach(), x.grad, [L.lam.grad for L in branch], [L.rho.grad for L in branch]))
+    (o1, g1, l1, r1) = grads[0]
     assert o1.shape == (3, 9, 256, 256)
-    assert torch.equal(o1, o2) and torch.equal(g1, g2)
-    assert all(torch.equal(a, b) for a, b in zip(l1, l2))
+    for (o2, g2, l2, r2) in grads[1:]:
+        assert torch.equal(o1, o2)
+        assert torch.allclose(g1, g2, rtol=1e-6, atol=1e-7 * float(g1.abs().max()))
+        assert all(torch.equal(a, b) for a, b in zip(l1, l2))
+        if train_rho:
+            assert all(torch.equal(a, b) for a, b in zip(r1, r2))
 
 
 @pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])

@@ -153,3 +153,25 @@ def test_mask_conditioned_oracle_equals_oracle_on_its_own_masks(iso):
         masks[1] = (m, sg)
     c = ot.tvd_fft_grads(y, lam, rho, h.astype(np.float64), iso, K, xbar, masks=masks)
     assert not np.allclose(a[1], c[1], rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("iso", [False, True])
+def test_split_gradients_and_term_scales(iso):
+    """tau as its own variable reproduces lambda_bar / rho_bar (lam_bar = tau_bar / rho, rho_bar =
+    rho_bar_explicit - tau_bar lam / rho^2), and the per-use copies of rho / tau (the term scales) change no
+    gradient; each scale bounds its sum from above."""
+    import torch
+    import oracle_torch as ot
+    from admm_deconv import synth
+    rng = np.random.default_rng(8)
+    h = synth.gaussian_psf(5, 1.0).astype(np.float64)
+    y = synth.make_batch(2, 20, 16, h.astype(np.float32), P=1).astype(np.float64)
+    xbar = rng.standard_normal(y.shape)
+    lam, rho, K = 0.02, 0.1, 5
+    _, yb, hb, lb, rb = ot.tvd_fft_grads(y, lam, rho, h, iso, K, xbar)
+    sc = {}
+    _, yb2, hb2, tb, re = ot.tvd_fft_grads_split(y, lam, rho, h, iso, K, xbar, scales=sc)
+    assert np.allclose(yb, yb2, rtol=1e-10, atol=1e-12) and np.allclose(hb, hb2, rtol=1e-10, atol=1e-12)
+    assert abs(tb / rho - lb) <= 1e-9 * abs(lb)
+    assert abs(re - tb * lam / rho ** 2 - rb) <= 1e-9 * max(abs(rb), 1.0)
+    assert sc["tau"] >= abs(tb) * (1 - 1e-12) and sc["rho"] >= abs(re) * (1 - 1e-12)
