@@ -1264,7 +1264,7 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
     L.hln = take(planes * MN * 4);
     L.sln = take(planes * MN * 8);
     if (rec) {
-        L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 8 : MN * 8));
+        L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 2 : MN * 8));
         L.sbar = take(planes * MN * 8);
         L.vsl = take(planes * MN * 4);
         L.part = take(planes * 16);

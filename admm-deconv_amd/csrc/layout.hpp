@@ -86,7 +86,7 @@ inline BwdHead bwd_head(int M, int N, size_t planes, int kh, int maxit, bool wan
     const int K = maxit < 1 ? 1 : maxit;
     const bool gen = generic_shape(M, N);
     const bool hq = want_h && kh > 0;
-    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 8 : 2 * MN * 4));
+    b.traj_s = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 2 : 2 * MN * 4));
     // forward dim-2 spectra per iteration: packed M/2 x N (power of two) or M/2+1 x N bins (generic)
     b.traj_v = hq ? take((size_t)K * planes * (gen ? (size_t)(M / 2 + 1) * N * 8 : MN * 4)) : 0;
     b.sig = hq ? take((size_t)(M / 2 + 1) * N * 16) : 0;

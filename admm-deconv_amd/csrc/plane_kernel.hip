@@ -819,14 +819,20 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         if constexpr (MASK) {
             // rho_bar is not formed in this mode (its <D vbar, D x_k> needs s_k itself): only the branch
             // decisions enter -- bitwise the same sbar and tau_bar as from the full trajectory
+            // Branch-free by construction (bit selects, no `m ? :`): from per-lane bits the compiler turned the
+            // selects into EXEC-masked branches, and the lane shifts (DPP) of neighbouring registers it
+            // scheduled into them then read inactive lanes.  Same values as the full path, bit for bit:
+            // sbar = m ? wbar : sbar_k - wbar;  tau_acc += m ? sgn (sbar_k - 2 wbar) : 0 (sgn = +-1: a sign flip).
             const unsigned byte = mwr[(n >> 2) & 1] >> (8 * (n & 3));
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const float wbv = rho * dv[c];
-                const bool m = (byte >> c) & 1u;
-                nb[c] = m ? wbv : b[c] - wbv;
-                const float sg = ((byte >> (4 + c)) & 1u) ? -1.0f : 1.0f;
-                tacc += m ? sg * (b[c] - 2.0f * wbv) : 0.0f;
+                const unsigned msk = 0u - ((byte >> c) & 1u);                 // all ones where |s| > tau
+                const unsigned sgb = ((byte >> (4 + c)) & 1u) << 31;          // sign bit of s
+                const unsigned keep = __float_as_uint(wbv), pass = __float_as_uint(b[c] - wbv);
+                nb[c] = __uint_as_float((keep & msk) | (pass & ~msk));
+                const unsigned tv = __float_as_uint(b[c] - 2.0f * wbv) ^ sgb;
+                tacc += __uint_as_float(tv & msk);
             }
             (void)a1;
             (void)a2;
