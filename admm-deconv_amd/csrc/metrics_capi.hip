@@ -34,7 +34,11 @@ struct Taps {
     int n;
 };
 
-__device__ __forceinline__ int wrapc(int i, int n) { return ((i % n) + n) % n; }   // circular (any offset)
+// circular index (any offset); in range -- the common case -- it is one compare, not two integer divisions
+__device__ __forceinline__ int wrapc(int i, int n) {
+    if ((unsigned)i < (unsigned)n) return i;
+    return ((i % n) + n) % n;
+}
 // NNlib pad_symmetric: ... b a | a b c | c b ...
 __device__ __forceinline__ int mirror(int i, int n) { return i < 0 ? -i - 1 : (i >= n ? 2 * n - i - 1 : i); }
 
@@ -347,20 +351,25 @@ __global__ __launch_bounds__(kT) void sqerr_kernel(const float* __restrict__ x, 
     block_sum_d2(acc, 0.0, part + 2 * ((size_t)plane * nblk + blockIdx.x));
 }
 
-// per image: sum the C * nblk partial pairs in a fixed order.
+// per image (one block each): sum the C * nblk partial pairs in a fixed order (thread t the strided
+// subset t, t + kT, ..., then the block's fixed-order tree).
 //   mode 0 (SSIM, MSE): out[b] = s1 / count
 //   mode 1 (GMSD): mu = s1/count, var = s2/count - mu^2, out[b] = sqrt(var); stats[b] = (mu, w_b / (count sqrt(var)))
-__global__ void reduce_img_kernel(const double* __restrict__ part, int per_img, double count, int mode,
-                                  float* __restrict__ out, float* __restrict__ stats, const float* __restrict__ wimg,
-                                  float wdef, int B) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    double s1 = 0.0, s2 = 0.0;
+__global__ __launch_bounds__(kT) void reduce_img_kernel(const double* __restrict__ part, int per_img, double count,
+                                                        int mode, float* __restrict__ out, float* __restrict__ stats,
+                                                        const float* __restrict__ wimg, float wdef, int B) {
+    const int b = blockIdx.x;
+    __shared__ double tot[2];
+    double a = 0.0, c = 0.0;
     const double* p = part + 2 * (size_t)b * per_img;
-    for (int i = 0; i < per_img; ++i) {
-        s1 += p[2 * i];
-        s2 += p[2 * i + 1];
+    for (int i = threadIdx.x; i < per_img; i += kT) {
+        a += p[2 * i];
+        c += p[2 * i + 1];
     }
+    block_sum_d2(a, c, tot);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const double s1 = tot[0], s2 = tot[1];
     if (mode == 0) {
         out[b] = (float)(s1 / count);
         return;
@@ -444,7 +453,7 @@ int admm_gmsd_f32(const float* x, const float* y, int M, int N, int C, int B, fl
     const dim3 g((M + TX - 1) / TX, (N + TY - 1) / TY, (unsigned)(C * B));
     hipLaunchKernelGGL(gmsd_fwd_kernel, g, dim3(kT), 0, s, x, y, M, N, t, alpha, part);
     if ((rc = launched())) return rc;
-    hipLaunchKernelGGL(reduce_img_kernel, dim3((B + 63) / 64), dim3(64), 0, s, part, C * L.nblk,
+    hipLaunchKernelGGL(reduce_img_kernel, dim3(B), dim3(kT), 0, s, part, C * L.nblk,
                        (double)M * N * C, 1, out, x_bar ? stats : nullptr, out_bar, 1.0f / B, B);
     if ((rc = launched())) return rc;
     if (x_bar) {
@@ -484,7 +493,7 @@ int admm_ssim_f32(const float* x, const float* y, int M, int N, int C, int B, co
                            coef, out_bar, C, 1.0f / B);
     }
     if ((rc = launched())) return rc;
-    hipLaunchKernelGGL(reduce_img_kernel, dim3((B + 63) / 64), dim3(64), 0, s, part, C * (int)(g.x * g.y),
+    hipLaunchKernelGGL(reduce_img_kernel, dim3(B), dim3(kT), 0, s, part, C * (int)(g.x * g.y),
                        (double)Mo * No * C, 0, out, nullptr, nullptr, 0.0f, B);
     if ((rc = launched())) return rc;
     if (x_bar) {
@@ -508,7 +517,7 @@ int admm_mse_f32(const float* x, const float* y, int M, int N, int C, int B, flo
     nblk = nblk < 1 ? 1 : (nblk > 64 ? 64 : nblk);
     hipLaunchKernelGGL(sqerr_kernel, dim3(nblk, C * B), dim3(kT), 0, s, x, y, MN, nblk, part);
     if ((rc = launched())) return rc;
-    hipLaunchKernelGGL(reduce_img_kernel, dim3((B + 63) / 64), dim3(64), 0, s, part, C * nblk, (double)MN * C, 0, out,
+    hipLaunchKernelGGL(reduce_img_kernel, dim3(B), dim3(kT), 0, s, part, C * nblk, (double)MN * C, 0, out,
                        nullptr, nullptr, 0.0f, B);
     return launched();
 }

@@ -733,15 +733,24 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
 #ifndef ADJX
 #define ADJX 0
 #endif
-template <bool MASK>
+// WV: the running sum Vsum of vbar is kept (y_bar or h_bar wanted); without it no Vsum instruction is issued
+// at all (zero-size resources would drop the traffic, but their loads still queue in the in-order vmcnt)
+template <bool MASK, bool WV>
 __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t s2p, rsrc_t sbl, rsrc_t sbs, rsrc_t vlp,
                                             rsrc_t vsp, unsigned vso, unsigned vss, float2* xb, float2* wb,
                                             float2* sink, float2* colbuf, int t, bool hb, bool lastk, float tau,
                                             float rho, float& racc, float& tacc) {
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
-    float4 s1r[2], s2r[2], sbr[2];
-    float2 vr[2];
+#ifndef ADJ_PD
+#define ADJ_PD 4
+#endif
+    // registers of loads in flight ahead of the one being processed: 4 (c5 one-grid reverse sweep 14.38 ->
+    // 13.29 ms against 1; 2: 13.78, 3: 13.49, 6: 13.60, 8: 13.42 and scratch in the full-trajectory variant)
+    constexpr int PD = ADJ_PD;
+    constexpr int NR = PD + 1;   // ring slots
+    float4 s1r[NR], s2r[NR], sbr[NR];
+    float2 vr[NR];
     unsigned mwr[2];   // MASK: s1p is the mask-bit slot of s_{k-1} (one dword per 4 registers)
     float2* stg = colbuf + t;
     float2* stg2 = stg + 16 * kPT;
@@ -756,14 +765,17 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
     const float v63y = stg2[15 * kPT].y;
     lds_barrier();
     sched_fence();
-    if constexpr (MASK) {
-        mwr[0] = bldu(s1p, t * 4, 0);
-    } else {
-        s1r[0] = bld4(s1p, t * 16, 0);
-        s2r[0] = bld4(s2p, t * 16, 0);
+    if constexpr (MASK) mwr[0] = bldu(s1p, t * 4, 0);
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        if constexpr (!MASK) {
+            s1r[i] = bld4(s1p, t * 16, i * kPT * 16);
+            s2r[i] = bld4(s2p, t * 16, i * kPT * 16);
+        }
+        sbr[i] = bld4(sbl, t * 16, i * kPT * 16);
+        if constexpr (WV) vr[i] = bld2(vlp, t * 8, i * kPT * 8);
+        else vr[i] = make_float2(0.f, 0.f);
     }
-    sbr[0] = bld4(sbl, t * 16, 0);
-    vr[0] = bld2(vlp, t * 8, 0);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
     float2* wbm = top ? wb + (w * 2 + hb) * 64 : sink + w * 128 + lane;
     float4 wc[2];
@@ -771,20 +783,21 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
     const float2 zero2 = make_float2(0.0f, 0.0f);
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
-        if (n + 1 < 64) {
-            const int q = (n + 1) & 1;
-            if constexpr (MASK) {
-                if (((n + 1) & 3) == 0) mwr[((n + 1) >> 2) & 1] = bldu(s1p, t * 4, ((n + 1) >> 2) * kPT * 4);
-            } else {
+        if constexpr (MASK) {   // the dword of the next 4 registers, PD registers ahead
+            if (n + PD < 64 && ((n + PD) & 3) == 0) mwr[((n + PD) >> 2) & 1] = bldu(s1p, t * 4, ((n + PD) >> 2) * kPT * 4);
+        }
+        if (n + PD < 64) {
+            const int q = (n + PD) % NR;
+            if constexpr (!MASK) {
                 __asm__ volatile("" ::"v"(s1r[q].x), "v"(s1r[q].y), "v"(s1r[q].z), "v"(s1r[q].w), "v"(s2r[q].x),
                                  "v"(s2r[q].y), "v"(s2r[q].z), "v"(s2r[q].w));
             }
-            __asm__ volatile("" ::"v"(sbr[q].x), "v"(sbr[q].y), "v"(sbr[q].z), "v"(sbr[q].w), "v"(vr[q].x),
-                             "v"(vr[q].y));
-            if (!MASK && !(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + 1) * kPT * 16);
-            if (!MASK && !(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + 1) * kPT * 16);
-            if (!(ADJX & 4)) sbr[q] = bld4(sbl, t * 16, (n + 1) * kPT * 16);
-            if (!(ADJX & 2)) vr[q] = bld2(vlp, t * 8, (n + 1) * kPT * 8);
+            __asm__ volatile("" ::"v"(sbr[q].x), "v"(sbr[q].y), "v"(sbr[q].z), "v"(sbr[q].w));
+            if constexpr (WV) __asm__ volatile("" ::"v"(vr[q].x), "v"(vr[q].y));
+            if (!MASK && !(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + PD) * kPT * 16);
+            if (!MASK && !(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + PD) * kPT * 16);
+            if (!(ADJX & 4)) sbr[q] = bld4(sbl, t * 16, (n + PD) * kPT * 16);
+            if (WV && !(ADJX & 2)) vr[q] = bld2(vlp, t * 8, (n + PD) * kPT * 8);
         }
         if (n == 32) {   // half-way: vbar[32..63] in, g[0..30] out (vbar[31] still pending in S[31])
 #pragma unroll
@@ -802,10 +815,10 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
             S[63] = stg2[15 * kPT];
             sched_fence();
         }
-        const float4 s1 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s1r[n & 1];
-        const float4 s2 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s2r[n & 1];
-        const float4 sb = sbr[n & 1];
-        const float2 vo = vr[n & 1];
+        const float4 s1 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s1r[n % NR];
+        const float4 s2 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s2r[n % NR];
+        const float4 sb = sbr[n % NR];
+        const float2 vo = vr[n % NR];
         const float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
         const float2 vub = xbp[n];
@@ -852,7 +865,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         // pin the accumulators here: left free, the compiler sinks the sums to the end of the
         // unrolled loop and keeps every register's operands live until then (~2000 VGPRs of spills)
         __asm__ volatile("" : "+v"(racc), "+v"(tacc));
-        if (!(ADJX & 2)) bst2(vsp, vso, n * vss, make_float2(vo.x + v.x, vo.y + v.y));
+        if (WV && !(ADJX & 2)) bst2(vsp, vso, n * vss, make_float2(vo.x + v.x, vo.y + v.y));
         const float4 nb4 = make_float4(nb[0], nb[1], nb[2], nb[3]);
         bst4(sbs, t * 16, n * kPT * 16, nb4);
         wbm[n] = make_float2(nb4.x, nb4.y);
@@ -903,7 +916,7 @@ __global__ __launch_bounds__(256) void dx_lane_kernel(const float* __restrict__ 
 //   part    : per plane (rho_bar partial, tau_bar partial) in fp64
 //   MASK    : traj is the mask-bit trajectory (plane256_kernel TRAJ 2; traj_slot in dwords); no dxK
 //   br      : several branches in one grid (x_bar in the chcat layout; vout, part per grid plane)
-template <bool MASK>
+template <bool MASK, bool WV>
 __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restrict__ xbar, const float* __restrict__ Cf,
                                                            const float* __restrict__ C0b,
                                                            const void* __restrict__ traj, size_t traj_slot,
@@ -961,7 +974,7 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         const rsrc_t sbs = k >= 2 ? make_rsrc(sbp, kS4) : none;
         // without vout (neither y_bar nor h_bar wanted) the Vsum accumulator is a zero-size resource: its
         // loads return 0 and its stores are dropped by the buffer unit, so it costs no HBM traffic
-        const bool wv = vout != nullptr;
+        const bool wv = WV;   // (launch_plane_adj picks WV = vout != NULL)
         const rsrc_t vlr = (k < K && wv) ? make_rsrc(vlp, kS2) : none;
         // the last step writes Vsum in the natural layout: byte r * 1024 + 16 n + 8 h
         const rsrc_t vsr = !wv ? none : k >= 2 ? make_rsrc(vlp, kS2) : make_rsrc(vout + plane * 65536, 65536 * 4);
@@ -969,7 +982,7 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         const unsigned vss = k >= 2 ? kPT * 8 : 16;
         float racc = 0.0f, tacc = 0.0f;
 #if !(ADJX & 1)
-        row_adjoint<MASK>(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
+        row_adjoint<MASK, WV>(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
                     tacc);
 #endif
         rsum += racc;

@@ -71,18 +71,17 @@ hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* t
                             hipStream_t s, const Branches* brp, bool masks) {
     const Tables t = carve(tables);
     const Branches br = brp ? *brp : one_branch();
-    if (masks) {
-        if (dxK) return hipErrorInvalidValue;   // rho_bar needs the full trajectory
-        (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBytes);
-        hipLaunchKernelGGL(plane256_adj_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
-                           t.C0b, traj, planes * 16 * kPT, dxK, sbar, vsl, vout, part, prm, K, br);
-    } else {
-        (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kLdsBytes);
-        hipLaunchKernelGGL(plane256_adj_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
-                           t.C0b, traj, planes * 64 * kPT, dxK, sbar, vsl, vout, part, prm, K, br);
+    if (masks && dxK) return hipErrorInvalidValue;   // rho_bar needs the full trajectory
+    const size_t slot = masks ? planes * 16 * kPT : planes * 64 * kPT;
+#define X(MK, WV)                                                                                              \
+    if (masks == MK && (vout != nullptr) == WV) {                                                             \
+        (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<MK, WV>,                                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);                \
+        hipLaunchKernelGGL((plane256_adj_kernel<MK, WV>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s,    \
+                           xbar, t.Cf, t.C0b, traj, slot, dxK, sbar, vsl, vout, part, prm, K, br);           \
     }
+    X(false, false) X(false, true) X(true, false) X(true, true)
+#undef X
     return hipGetLastError();
 }
 
