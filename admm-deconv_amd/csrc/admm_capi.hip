@@ -351,6 +351,7 @@ struct Traj {
     double2* sig = nullptr;  // (M/2+1) x N                 : top-left PSF spectrum (h_bar only)
     float* nrm = nullptr;    // (K-1) x M x N               : isotropic batch norm of s_k (iso only)
     unsigned* m = nullptr;   // (K-1) x planes x 16 x 512   : ST mask bytes of s_k instead of s (fused only)
+    bool iso_lane = false;   // isotropic 256 x 256: s and nrm lane-native (plane_iso.hip), for the fused adjoint
 };
 
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
@@ -463,6 +464,32 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                                    opt(ADMM_OPT_PLANE_STAGGER), nullptr, tr.m);
         });
         return rc;
+    }
+    if (iso && fused_tables_shape(M, N) && !red && (!tr.s || tr.iso_lane) && !tr.v && fused_enabled()) {
+        // isotropic at 256 x 256: the split-iteration per-plane kernels (plane_iso.hip), the spectrum
+        // resident in the CU; per iteration one plane256_iso_kernel and one iso_norm_kernel (batch norm)
+        namespace pk = admm::plane;
+        void* tables = ws + lay.F;
+        rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, tables, s); });
+        if (rc) return rc;
+        float2* fl = reinterpret_cast<float2*>(ws + lay.fmap);
+        float2* ql = reinterpret_cast<float2*>(spec1);
+        // recording: s_{k+1} into trajectory slot k, |s_{k+1}| into norm slot k (lane-native)
+        float4* st = reinterpret_cast<float4*>(tr.iso_lane ? tr.s : sbuf[0]);
+        const size_t tslot = tr.iso_lane ? planes * MN / 2 : 0;   // float4 per slot
+        for (int k = 0; k < maxit; ++k) {
+            rc = ln.run(ADMM_K_PLANE, [&] {
+                return pk::launch_plane_iso(y, x_out, tables, kh > 0, spec0, st + (k > 0 ? (size_t)(k - 1) * tslot : 0),
+                                            st + (size_t)k * tslot, fl, ql, prm, k, maxit, planes, s);
+            });
+            if (rc) return rc;
+            if (k + 1 < maxit) {
+                float2* nr = tr.iso_lane ? reinterpret_cast<float2*>(tr.nrm + (size_t)k * MN) : nullptr;
+                rc = ln.run(ADMM_K_NORM, [&] { return pk::launch_iso_norm(ql, fl, nr, prm, planes, s); });
+                if (rc) return rc;
+            }
+        }
+        return ADMM_OK;
     }
     const int T = line_T(M, N);
     const int KB = column_KB(M, N);
@@ -743,6 +770,7 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
         b.nblk_isoA = (int)(ng * gen_nb(N, T));
         b.nblk_isoR = kIsoAdjRBlocks;
         b.nblk_line = b.nblk_isoA + b.nblk_isoR;
+        if (b.nblk_line < 512) b.nblk_line = 512;   // the fused sweep's 512 tau_bar rows per step (plane_iso.hip)
     } else {
         b.nblk_line = (int)(planes * gen_nb(N, T));
     }
@@ -928,14 +956,18 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
     // mask-bit trajectory (ADMM_REC_MASKS, fused forward + fused reverse sweep): asked for by a recording,
     // and taken by the combined call whenever rho_bar is not wanted
-    const bool masks_ok = ln_traj && !iso && fused_adj_enabled();
+    // isotropic at 256 x 256: the split-iteration fused forward records s and |s| lane-native for the fused
+    // reverse sweep (plane_iso.hip) -- also without rho_bar, so the same flag selects it
+    const bool iso_ok = iso && fused_tables_shape(M, N) && !red && !want_h && fused_enabled() && fused_adj_enabled();
+    const bool masks_ok = (ln_traj && !iso && fused_adj_enabled()) || iso_ok;
     bool use_masks = masks_ok && (phases == 1 ? (rec_flags & ADMM_REC_MASKS) != 0 : rho_bar == nullptr);
     if (phases == 2) {
         std::lock_guard<std::mutex> lk(g_rec_mu);
         auto it = g_rec.find(workspace);
         use_masks = it != g_rec.end() && it->second.masks != 0;
     }
-    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0, use_masks);
+    const bool iso_lane = use_masks && iso;   // the fused isotropic sweep (no mask bits: s itself is needed)
+    const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0, use_masks && !iso);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
     RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h, sc);
@@ -950,8 +982,8 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
             return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request, "
                                         "lambda / rho or library options changed between record and replay)");
         if (use_masks && rho_bar)
-            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only): rho_bar cannot be "
-                                        "formed from it; record without the flag to get rho_bar");
+            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only / the fused isotropic "
+                                        "trajectory): rho_bar cannot be formed from it; record without the flag to get rho_bar");
         g_rec.erase(it);
     } else {
         std::lock_guard<std::mutex> lk(g_rec_mu);
@@ -990,7 +1022,8 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     // ---- forward with trajectory ----
     Traj tr;
     tr.s = reinterpret_cast<float*>(ws + bl.traj_s);
-    tr.m = use_masks ? reinterpret_cast<unsigned*>(ws + bl.traj_s) : nullptr;
+    tr.m = use_masks && !iso ? reinterpret_cast<unsigned*>(ws + bl.traj_s) : nullptr;
+    tr.iso_lane = iso_lane;
     tr.v = want_h ? reinterpret_cast<float2*>(ws + bl.traj_v) : nullptr;
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
@@ -1039,6 +1072,34 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
         });
         if (rc) return rc;
         red_rows = (int)planes;
+    } else if (iso_lane) {
+        // isotropic fused sweep: per step one plane256_isoadj_kernel (B phase of step k+1, column phase, A phase
+        // of step k) and one iso_radj_kernel (R_k over the batch, tau_bar rows); rows of step k at (K - k) x 512
+        namespace pk = admm::plane;
+        const size_t kE = MN / 2;   // lane-native float2 elements per plane
+        float4* trs = reinterpret_cast<float4*>(tr.s);
+        const float2* trn = reinterpret_cast<const float2*>(tr.nrm);
+        float2* vbuf = reinterpret_cast<float2*>(ws + bl.wbar);
+        float2* rmap = reinterpret_cast<float2*>(ws + bl.Rmap);
+        float2* rpl = specB;    // per plane R partials (the forward's q partials, free now)
+        float2* vsl = specA;    // lane-native Vsum (the forward's H^T y, free now)
+        float* vout = !want_v ? nullptr : kh > 0 ? vsum : y_bar;
+        HIPCHK(hipMemsetAsync(rpart, 0, (size_t)(K > 1 ? K - 1 : 1) * 512 * 2 * 8, s));
+        for (int k = K; k >= 1; --k) {
+            rc = ln.run(ADMM_K_ADJ, [&] {
+                return pk::launch_plane_isoadj(x_bar, ws + bl.f.F, trs, planes * kE, trn, kE, vbuf,
+                                               reinterpret_cast<float4*>(sb[0]), rmap, rpl, vsl, vout, prm, k, K, planes, s);
+            });
+            if (rc) return rc;
+            if (k >= 2) {
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    return pk::launch_iso_radj(rpl, rmap, trn + (size_t)(k - 2) * kE, rpart + (size_t)(K - k) * 512 * 2, 0,
+                                               prm, planes, s);
+                });
+                if (rc) return rc;
+            }
+        }
+        red_rows = (K > 1 ? K - 1 : 1) * 512;
     } else if (want_v) {
         HIPCHK(hipMemsetAsync(vsum, 0, planes * MN * 4, s));
     }
@@ -1047,7 +1108,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     float* Rpart = iso ? reinterpret_cast<float*>(ws + bl.Rpart) : nullptr;
     const int ngi = iso_ngroups(planes);
     // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
-    if (iso) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
+    if (iso && !iso_lane) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
     if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
     if (gen) {
         // ---- runtime-length reverse sweep (admm_generic_bwd.hip): column, line inverse -> vbar_k in
@@ -1111,11 +1172,11 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
             });
             if (rc) return rc;
         }
-    } else if (!fused_adj) {
+    } else if (!fused_adj && !iso_lane) {
         rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N); });
         if (rc) return rc;
     }
-    for (int k = (fused_adj || gen) ? 0 : K; k >= 1; --k) {
+    for (int k = (fused_adj || gen || iso_lane) ? 0 : K; k >= 1; --k) {
         float2* vs = want_h ? tr.v + (size_t)(k - 1) * planes * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
             return launch_column(N, want_h ? 4 : 0, gc, clds, s, specA, specB, Ct, Gt, twN, L, KB, 1.0f, vs, Qp);
@@ -1220,7 +1281,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
             });
             if (rc) return rc;
         }
-    } else if (!fused_adj && y_bar) {   // (the fused sweep wrote Vsum straight into y_bar)
+    } else if (!fused_adj && !iso_lane && y_bar) {   // (the fused sweeps wrote Vsum straight into y_bar)
         HIPCHK(hipMemcpyAsync(y_bar, vsum, planes * MN * 4, hipMemcpyDeviceToDevice, s));
     }
     rc = ln.run(ADMM_K_FINAL, [&] {

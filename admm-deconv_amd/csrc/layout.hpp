@@ -15,6 +15,8 @@ inline bool pow2_shape(int M, int N) { return is_pow2(M) && is_pow2(N) && M >= 4
 inline bool generic_shape(int M, int N) { return !pow2_shape(M, N); }
 // The fused per-plane kernel (plane_kernel.hip) covers 256 x 256 planes with the anisotropic prox.
 inline bool fused_shape(int M, int N, bool iso) { return M == 256 && N == 256 && !iso; }
+// The isotropic split-iteration kernels (plane_iso.hip) cover 256 x 256 as well; both need the lane-native tables.
+inline bool fused_tables_shape(int M, int N) { return M == 256 && N == 256; }
 inline size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
 // Planes per isotropic plane-group block (ISO_A / ISO_ADJ_A keep a group's partial batch sums in
@@ -56,7 +58,7 @@ inline Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.xg = generic_shape(M, N) ? take(planes * MN * 4) : 0;
     L.fmap = iso ? take(MN * 4) : 0;
     L.part = iso ? take((size_t)iso_ngroups(planes) * MN * 4) : 0;
-    L.F = fused_shape(M, N, iso) ? take(admm::plane::tables_bytes()) : 0;
+    L.F = fused_tables_shape(M, N) ? take(admm::plane::tables_bytes()) : 0;
     L.total = off;
     return L;
 }

@@ -170,6 +170,15 @@ __device__ __forceinline__ float phi_tau(float s, float tau) {
 #endif
 }
 
+// Materialise every S register at a phase boundary.  Without it the compiler moves the tail of a line
+// transform past the next phase's LDS traffic in straight-line code, and the overlap of the two register
+// peaks spills (the isotropic kernel: 376 B per lane; inside plane256_kernel's loop the back-edge separates
+// them, except in the PSF prologue).
+__device__ __forceinline__ void pin_regs(float2 (&S)[64]) {
+#pragma unroll
+    for (int n = 0; n < 64; ++n) __asm__ volatile("" : "+v"(S[n].x), "+v"(S[n].y));
+}
+
 // Lane-native spectral tables, built once per call from the 2-pass tables Ct/Gt (bin (kj, k) at
 // kj*(M/2+1) + k).  Entry ((half*4 + i)*8 + q2)*512 + t is the multiplier thread t applies to bin
 // kj = q + 8 i + 32 q2 (q = t & 7) of spectral column k = 32 half + (c >> 1) + 64 (c & 1), c = t >> 3.
@@ -635,6 +644,9 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     const rsrc_t gfr = make_rsrc(Gf, PSF ? kTab * 8 : 0);
     if constexpr (PSF) {
         line_forward_pair(S, hb);
+#ifndef PLANE_NO_PIN
+        pin_regs(S);
+#endif
         column_phase<1>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
         // = H^T y (the 1/(MN) is in Gf).  Staged as in the iterations (x[32..63] through per-thread LDS
         // slots, no barrier): the unstaged inverse's peak exceeds 256 VGPRs and spilled.

@@ -2,6 +2,7 @@
 // see plane_api.hpp) and its host launchers.
 #include "plane_api.hpp"
 #include "plane_kernel.hip"
+#include "plane_iso.hip"
 
 namespace admm {
 namespace plane {
@@ -82,6 +83,60 @@ hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* t
     }
     X(false, false) X(false, true) X(true, false) X(true, true)
 #undef X
+    return hipGetLastError();
+}
+
+hipError_t launch_plane_iso(const float* y, float* x_out, const void* tables, bool psf, float2* hln, const float4* s_in,
+                            float4* s_out, const float2* fmap, float2* qpart, const float* prm, int k, int K,
+                            size_t planes, hipStream_t s, const Branches* brp) {
+    const Tables t = carve(tables);
+    const Branches br = brp ? *brp : one_branch();
+    if (psf) {
+        (void)hipFuncSetAttribute((const void*)plane256_iso_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_iso_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf,
+                           t.C0b, t.Gf, t.G0b, hln, s_in, s_out, fmap, qpart, prm, k, K, br);
+    } else {
+        (void)hipFuncSetAttribute((const void*)plane256_iso_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_iso_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out, t.Cf,
+                           t.C0b, t.Gf, t.G0b, hln, s_in, s_out, fmap, qpart, prm, k, K, br);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_iso_norm(const float2* qpart, float2* fmap, float2* nrm, const float* prm, size_t planes,
+                           hipStream_t s, const Branches* brp) {
+    const Branches br = brp ? *brp : Branches{(int)planes, 1, 1, 0u, 0u};
+    hipLaunchKernelGGL(iso_norm_kernel, dim3(64 * kPT / 64, (unsigned)br.nbr), dim3(256), 0, s, qpart, fmap, nrm, prm, br);
+    return hipGetLastError();
+}
+
+hipError_t launch_plane_isoadj(const float* xbar, const void* tables, const float4* traj, size_t tslot, const float2* nrm,
+                               size_t nslot, float2* vbuf, float4* sbar, const float2* Rmap, float2* rpart, float2* vsl,
+                               float* vout, const float* prm, int k, int K, size_t planes, hipStream_t s,
+                               const Branches* brp) {
+    const Tables t = carve(tables);
+    const Branches br = brp ? *brp : one_branch();
+    if (vout) {
+        (void)hipFuncSetAttribute((const void*)plane256_isoadj_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_isoadj_kernel<true>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
+                           t.C0b, traj, tslot, nrm, nslot, vbuf, sbar, Rmap, rpart, vsl, vout, prm, k, K, br);
+    } else {
+        (void)hipFuncSetAttribute((const void*)plane256_isoadj_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kLdsBytes);
+        hipLaunchKernelGGL(plane256_isoadj_kernel<false>, dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, xbar, t.Cf,
+                           t.C0b, traj, tslot, nrm, nslot, vbuf, sbar, Rmap, rpart, vsl, vout, prm, k, K, br);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_iso_radj(const float2* rpart, float2* Rmap, const float2* nrm1, double* part, size_t part_branch,
+                           const float* prm, size_t planes, hipStream_t s, const Branches* brp) {
+    const Branches br = brp ? *brp : Branches{(int)planes, 1, 1, 0u, 0u};
+    hipLaunchKernelGGL(iso_radj_kernel, dim3(64 * kPT / 64, (unsigned)br.nbr), dim3(256), 0, s, rpart, Rmap, nrm1, part,
+                       part_branch, prm, br);
     return hipGetLastError();
 }
 

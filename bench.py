@@ -110,6 +110,24 @@ def make_inputs(cfg, B, g0, distinct, dev):
             psf, base)
 
 
+def iso_fused_bytes_per_px(K):
+    """HBM bytes per pixel of one isotropic solve's plane256_iso_kernel launches (all K) and plane256_isoadj_kernel
+    launches (all K; no y_bar, no rho_bar: the c5 layers' case) -- DESIGN.md s3.
+    Forward: k = 0 y in, H^T y out, s_1 out, q out (4 + 4 + 8 + 4); 0 < k < K-1: H^T y, s_k (B phase), s_k
+    again, s_{k+1}, q (A phase) (4 + 8 + 8 + 8 + 4); k = K-1: H^T y, s_k, x out (4 + 8 + 4).
+    Reverse step k: B phase (k < K) vbar_{k+1} in, s_k in, sbar_{k+1} in (k + 1 < K), sbar_k out (4 + 8 + 8 + 8);
+    k = K: x_bar in (4); A phase (k >= 2) vbar_k out, s_{k-1} in, sbar_k in (k < K), R partial out (4 + 8 + 8 + 4)."""
+    if K == 1:
+        return 8.0, 4.0
+    fwd = 20 + 32 * (K - 2) + 16
+    adj = 0
+    for k in range(K, 0, -1):
+        adj += 4 if k == K else 4 + 8 + (8 if k + 1 < K else 0) + 8
+        if k >= 2:
+            adj += 4 + 8 + (8 if k < K else 0) + 4
+    return float(fwd), float(adj)
+
+
 def bench_c5(args, dev):
     """BASELINE c5: the denoiser branch of src/nets/net_build.jl:113-128 (5 x ADMMDeconvF2((), 50, rho, relu1)
     in Parallel(chcat)), batch 64 of 256x256 RGB; one step = forward + GMSD loss + backward through the HIP
@@ -186,6 +204,24 @@ def bench_c5(args, dev):
         roof = {"bound": "hbm", "kernel": f"{dom} (one grid of {nb} branches x {planes} planes)", "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic("c5m", dom), "algorithmic_bytes_per_launch": per[dom],
+                "avg_launch_ms": round(a["avg_ms"], 5)}
+    elif args.iso and kernels.get("plane", {}).get("launches_per_step") == len(branch) * K:
+        # isotropic at 256 x 256: the split-iteration kernels of plane_iso.hip, one plane256_iso_kernel per
+        # iteration and one plane256_isoadj_kernel per reverse step (the batch norm / R sums between them are
+        # "norm").  Per pixel of a launch (the branch's 256 KiB f / R / |s| maps are L2-resident, not counted):
+        fwd, adj = iso_fused_bytes_per_px(K)
+        nb = len(branch)
+        per = {"plane": planes * M * N * fwd / K, "adjoint": planes * M * N * adj / K}
+        for k, b in per.items():
+            if k in kernels:
+                kernels[k]["algorithmic_bytes_per_launch"] = b
+                kernels[k]["achieved_GBps"] = round(b / (kernels[k]["avg_ms"] * 1e-3) / 1e9, 1)
+        dom = max((k for k in per if k in kernels), key=lambda k: kernels[k]["total_ms_per_step"])
+        a = kernels[dom]
+        ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": f"{dom} (plane_iso.hip, {nb} branches x {K} launches)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic("c5iso", dom), "algorithmic_bytes_per_launch": per[dom],
                 "avg_launch_ms": round(a["avg_ms"], 5)}
     elif not args.iso and kernels.get("adjoint", {}).get("launches_per_step") == len(branch):
         # fused reverse sweep (plane256_adj_kernel, one launch per layer).  The input and rho need no gradient,

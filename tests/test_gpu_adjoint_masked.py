@@ -18,7 +18,7 @@ summation is judged; where a gradient's arithmetic is ill-conditioned beyond tha
 tau / |s|^3 just above the threshold), the bound is 3x the error of an fp32 torch evaluation of the SAME
 mask-conditioned computation.
 Every reverse-sweep variant: 2-pass (power-of-two), fused trajectory + 2-pass sweep, fused sweep, the
-runtime-length sweep, isotropic; incl. the c4 plane at K = 50, the c5 layer shape (256^2 x 3, K = 50) and
+runtime-length sweep, isotropic (2-pass and the fused 256 x 256 sweep of plane_iso.hip); incl. the c4 plane at K = 50, the c5 layer shape (256^2 x 3, K = 50) and
 the case profiles/r02_grad_bounds.txt:5 flagged (128^2, 10x10 random PSF, K = 5)."""
 import contextlib
 import ctypes
@@ -92,6 +92,13 @@ def lane_native_to_natural(a, planes):
     return a.reshape(-1, planes, 2, 256, 256)
 
 
+def lane_native_map_to_natural(a):
+    """Lane-native per-pixel maps, K' x (64 registers, 512 threads, 2) -> (K', 256, 256): entry [n][t = 2r + h]
+    holds pixels p = 4n + 2h and p + 1 of line r (plane_iso.hip)."""
+    a = np.asarray(a).reshape(-1, 64, 256, 2, 2)                 # [k][n][r][h][e]
+    return a.transpose(0, 2, 1, 3, 4).reshape(-1, 256, 256)
+
+
 def read_trajectory(rec, K, lane_native):
     """(s_1..s_{K-1} as (K-1, B, P, 2, N, M) fp32, |s_k| maps (K-1, N, M) or None) of a recording."""
     M, N, P, B, kh, kw = rec.dims
@@ -109,7 +116,8 @@ def read_trajectory(rec, K, lane_native):
     nrm = None
     if rec.iso:
         m = (K - 1) * M * N
-        nrm = buf[base + tn.value: base + tn.value + 4 * m].view(torch.float32).cpu().numpy().reshape(K - 1, N, M)
+        nrm = buf[base + tn.value: base + tn.value + 4 * m].view(torch.float32).cpu().numpy()
+        nrm = lane_native_map_to_natural(nrm.reshape(K - 1, -1)) if lane_native else nrm.reshape(K - 1, N, M)
     return s, nrm
 
 
@@ -130,7 +138,7 @@ def _scalar_rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
 
 
-def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned=False):
+def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned=False, need_rho=True):
     """GPU record + replay, the trajectory's masks, and the errors against the mask-conditioned fp64 oracle
     (and, as the arithmetic reference, of an fp32 torch evaluation of the same mask-conditioned computation)."""
     B, P, N, M = y.shape
@@ -139,15 +147,18 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     with contextlib.ExitStack() as st:
         for k, v in opts.items():
             st.enter_context(_lib.option(k, v))
-        lane_native = (M == 256 and N == 256 and not iso and not (need_h and h is not None)
-                       and _lib.get_option("FUSED") == 1)
-        x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, iso, K, need_h=need_h)
+        # need_rho=False records masks (anisotropic: not a trajectory of s, so not used here) or, isotropic at
+        # 256 x 256, the fused sweep's lane-native s and |s| (plane_iso.hip)
+        assert need_rho or iso
+        fused = M == 256 and N == 256 and not (need_h and h is not None) and _lib.get_option("FUSED") == 1
+        lane_native = fused and (not iso or (not need_rho and _lib.get_option("FUSED_ADJ") == 1))
+        x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, iso, K, need_h=need_h, need_rho=need_rho)
         torch.cuda.synchronize()
         masks = []
         if K > 1:
             s_traj, nrm = read_trajectory(rec, K, lane_native)
             masks = oracle_torch.masks_from_trajectory(s_traj, lam, rho, iso, nrm)
-        yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt)
+        yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt, need_rho=need_rho)
         torch.cuda.synchronize()
     lam32, rho32 = np.float32(lam), np.float32(rho)
     h64 = None if h is None else h.astype(np.float64)
@@ -164,15 +175,19 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     _, yb32, hb32, lb32, rb32 = oracle_torch.tvd_fft_grads(y, lam32, rho32, h, iso, K, xbar, dtype=torch.float32,
                                                            masks=masks)
     err = {"x": _plane_rel(x.cpu().numpy(), x0), "y_bar": _plane_rel(yb.cpu().numpy(), yb0),
-           "lambda_bar": abs(float(lb) - lb0) / max(lam_scale, 1e-300),
-           "rho_bar": abs(float(rb) - rb0) / max(rho_scale, 1e-300)}
+           "lambda_bar": abs(float(lb) - lb0) / max(lam_scale, 1e-300)}
+    if need_rho:
+        err["rho_bar"] = abs(float(rb) - rb0) / max(rho_scale, 1e-300)
+    else:
+        assert rb is None
     ref32 = {"y_bar": _plane_rel(yb32, yb0), "lambda_bar": abs(lb32 - lb0) / max(lam_scale, 1e-300),
              "rho_bar": abs(rb32 - rb0) / max(rho_scale, 1e-300)}
     if hb is not None:
         err["h_bar"] = _rel(hb.cpu().numpy(), hb0)
         ref32["h_bar"] = _rel(hb32, hb0)
     info = {"rho_bar": rb0, "rho_bar_scale": rho_scale, "lambda_bar": lb0, "lambda_bar_scale": lam_scale,
-            "rel_to_value": {"lambda_bar": _scalar_rel(float(lb), lb0), "rho_bar": _scalar_rel(float(rb), rb0)}}
+            "rel_to_value": {"lambda_bar": _scalar_rel(float(lb), lb0),
+                             "rho_bar": _scalar_rel(float(rb), rb0) if need_rho else None}}
     if K > 1:
         # the masks' distance from the oracle's own fp64 forward: how many bits the conditioning moved
         rec64 = []
@@ -186,7 +201,7 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     if unconditioned:
         _, ybu, hbu, lbu, rbu = oracle_torch.tvd_fft_grads(y.astype(np.float64), lam32, rho32, h64, iso, K, xbar)
         info["unconditioned"] = {"y_bar": _plane_rel(yb.cpu().numpy(), ybu), "lambda_bar": _scalar_rel(float(lb), lbu),
-                                 "rho_bar": _scalar_rel(float(rb), rbu)}
+                                 "rho_bar": _scalar_rel(float(rb), rbu) if need_rho else None}
         if hb is not None:
             info["unconditioned"]["h_bar"] = _rel(hb.cpu().numpy(), hbu)
     out = os.environ.get("ADMM_GRAD_LOG")
@@ -215,6 +230,47 @@ def test_adjoint_vs_mask_conditioned_oracle(dev, case):
     xbar = rng.standard_normal(y.shape).astype(np.float32)
     err, ref32 = run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts)
     check(cid, err, ref32)
+
+
+# the fused isotropic reverse sweep (plane_iso.hip): recorded without rho_bar, lane-native s and |s|
+ISO_FUSED_CASES = [
+    # (id, B, P, psf, lam, rho, K)
+    ("isofused-256-c5layer-K50", 2, 3, None, 0.0041, 0.021, 50),
+    ("isofused-256-psf-K25", 2, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
+    ("isofused-256-1plane-K7", 1, 1, ("rand", 7, 4), 0.02, 0.1, 7),
+    ("isofused-256-K2", 3, 1, None, 0.01, 0.05, 2),
+    ("isofused-256-K1", 2, 1, None, 0.01, 0.05, 1),
+]
+
+
+@pytest.mark.parametrize("case", ISO_FUSED_CASES, ids=[c[0] for c in ISO_FUSED_CASES])
+def test_fused_iso_adjoint_vs_mask_conditioned_oracle(dev, case):
+    cid, B, P, spec, lam, rho, K = case
+    rng = np.random.default_rng(K + 31 * B + 7 * P)
+    h = _psf(spec, rng)
+    y = synth.make_batch(B, 256, 256, h, P=P, g0=5)
+    xbar = rng.standard_normal(y.shape).astype(np.float32)
+    err, ref32 = run_case(dev, cid, y, xbar, h, lam, rho, K, True, False, {}, need_rho=False)
+    check(cid, err, ref32)
+
+
+def test_fused_iso_adjoint_deterministic_and_combined(dev):
+    """Two recordings + replays bitwise equal (fixed-order batch sums); the combined call without rho_bar takes
+    the same fused sweep (bitwise), with rho_bar the 2-pass sweep (same lambda_bar to rounding)."""
+    y = torch.from_numpy(synth.make_batch(2, 256, 256, None, P=3, g0=3)).to(dev)
+    xb = torch.randn_like(y)
+    outs = []
+    for _ in range(2):
+        x, rec = admm_deconv.tvd_fft_record(y, 0.0041, 0.021, None, True, 20, need_rho=False)
+        outs.append((x,) + admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_rho=False)[:3:2])
+    c = admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, None, True, 20, need_rho=False)
+    full = admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, None, True, 20)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(*outs))
+    assert torch.equal(c[0], outs[0][0]) and torch.equal(c[1], outs[0][1]) and torch.equal(c[3], outs[0][2])
+    assert full[4] is not None
+    assert abs(float(full[3]) - float(c[3])) <= 1e-3 * abs(float(full[3]))
+    assert float((full[1] - c[1]).norm() / full[1].norm()) <= 1e-3
 
 
 def test_grad_bounds_outlier_case(dev):
