@@ -42,7 +42,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
 REC_HBAR, REC_MASKS = 1, 2
-MULTI_RECORD = 1
+MULTI_RECORD, MULTI_ISO = 1, 4
 
 
 # admm_reduce_fn / admm_batch_reducer (include/admm_deconv.h): cross-shard sum of an M x N map

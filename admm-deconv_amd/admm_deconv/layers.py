@@ -211,7 +211,7 @@ class Parallel:
     branch sees the same input and `connection` combines the branch outputs.
 
     When every branch is an ADMM layer the one-grid solve covers (the denoiser: ADMMDeconvF2((), K, ρ_i, σ),
-    anisotropic, 256 x 256, same K), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
+    256 x 256, same K and prox; isotropic only with merge="always" and no ρ needing a gradient), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
     planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
     each branch's bias and σ then apply to its slice.  Results are bitwise those of the branches run one
     by one.  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
@@ -223,7 +223,7 @@ class Parallel:
         self.connection = connection
         self.layers = list(layers)
         self.use_streams = bool(streams)
-        self.merge = bool(merge)
+        self.merge = merge if merge == "always" else bool(merge)
         self._streams = {}
 
     def _mergeable(self, x):
@@ -232,16 +232,26 @@ class Parallel:
         Ls = self.layers
         if not all(isinstance(L, Admm) for L in Ls):
             return False
-        K = Ls[0].iters
-        return all(L.iters == K and not L.iso and L.weight.numel() == 0 and L.group is None for L in Ls) and \
-            multi_supported(x)
+        K, iso = Ls[0].iters, Ls[0].iso
+        # isotropic: only on request (merge="always").  Its one-grid solve is a launch per iteration either way,
+        # and the branches on their own streams overlap one branch's batch-norm launches with the others'
+        # plane launches: c5 iso 1.10k img/s per-branch against 0.97k in one grid (profiles/r03_c5iso_*.json).
+        # It forms no rho_bar either.
+        if iso and (self.merge != "always" or any(self._needs_rho(L) for L in Ls)):
+            return False
+        return all(L.iters == K and L.iso == iso and L.weight.numel() == 0 and L.group is None for L in Ls) and \
+            multi_supported(x, iso)
+
+    @staticmethod
+    def _needs_rho(L):
+        return torch.is_grad_enabled() and isinstance(L.rho, torch.Tensor) and L.rho.requires_grad
 
     def _merged(self, x):
         """All branches in one solve (ops.tvd_fft_multi); bias and σ per branch, then the connection."""
         Ls = self.layers
         for L in Ls:
             L.project()          # deconv_admm.jl:216-219, in place on the device
-        xa = tvd_fft_multi_grad(x, [L.lam for L in Ls], [L.rho for L in Ls], Ls[0].iters)
+        xa = tvd_fft_multi_grad(x, [L.lam for L in Ls], [L.rho for L in Ls], Ls[0].iters, Ls[0].iso)
         P = x.shape[1]
         if self.connection is chcat and all(L.bias is False and L.sigma is Ls[0].sigma for L in Ls):
             return Ls[0].sigma(xa)   # σ elementwise over the whole chcat tensor: the same values, no copies

@@ -427,9 +427,11 @@ MULTI_M = MULTI_N = 256
 
 def multi_supported(y, isotropic=False, psf=None, group=None):
     """Whether the one-grid multi-branch solve (admm_tvd_forward_multi_dev_f32) covers this input: the fused
-    256 x 256 anisotropic kernel, no PSF, one process holding the batch, and the fused option on."""
+    256 x 256 kernels (anisotropic, or isotropic with the fused reverse sweep on), no PSF, one process
+    holding the batch, and the fused option on."""
     return (isinstance(y, torch.Tensor) and y.is_cuda and y.dtype == torch.float32 and y.dim() == 4
-            and y.shape[-1] == MULTI_M and y.shape[-2] == MULTI_N and not isotropic
+            and y.shape[-1] == MULTI_M and y.shape[-2] == MULTI_N
+            and (not isotropic or _lib.get_option("FUSED_ADJ") == 1)
             and (psf is None or psf.numel() == 0) and group is None and _lib.get_option("FUSED") == 1)
 
 
@@ -442,14 +444,19 @@ def _ptr_array(ts):
     return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
 
-def tvd_fft_multi(y, lams, rhos, maxit=100, *, out=None, record=False, need_rho=True, workspace=None, stream=None):
+def tvd_fft_multi(y, lams, rhos, maxit=100, *, out=None, record=False, need_rho=True, isotropic=False, workspace=None,
+                  stream=None):
     """x = chcat(tvd_fft(y, lams[0], rhos[0], nothing, false, maxit), ..., tvd_fft(y, lams[n-1], ...)) in ONE
     launch of the fused kernel (every branch's planes in one grid).  y: (B, P, 256, 256) float32 on the
     device; lams, rhos: n 1-element tensors / numbers (device tensors read in-kernel).  Returns x of shape
     (B, n * P, 256, 256) -- the chcat layout, branch i's channels at i*P..i*P+P-1 -- and, with record=True,
-    a MultiRecording for tvd_fft_multi_backward_recorded (need_rho=False: only the ST branches are kept)."""
-    if not multi_supported(y):
-        raise ValueError("tvd_fft_multi: y must be a float32 (B, P, 256, 256) ROCm tensor (fused option on)")
+    a MultiRecording for tvd_fft_multi_backward_recorded (need_rho=False: only the ST branches are kept).
+    isotropic=True: the BT prox (ops.jl:6,10), each branch's norm over its own planes; its recording never
+    gives rho_bar (the fused isotropic sweep, plane_iso.hip)."""
+    if not multi_supported(y, isotropic):
+        raise ValueError("tvd_fft_multi: y must be a float32 (B, P, 256, 256) ROCm tensor (fused options on)")
+    if record and isotropic and need_rho:
+        raise ValueError("tvd_fft_multi: an isotropic recording gives lambda_bar and y_bar only (need_rho=False)")
     n = len(lams)
     if n < 1 or len(rhos) != n:
         raise ValueError("tvd_fft_multi: one lambda and one rho per branch")
@@ -458,6 +465,8 @@ def tvd_fft_multi(y, lams, rhos, maxit=100, *, out=None, record=False, need_rho=
     stream, s_handle = _stream_of(stream, y.device)
     dv = [_DevScalars(l, r, y.device, stream) for l, r in zip(lams, rhos)]
     flags = (_lib.MULTI_RECORD | (0 if need_rho else _lib.REC_MASKS)) if record else 0
+    if isotropic:
+        flags |= _lib.MULTI_ISO
     nbytes = _lib.multi_workspace_bytes(M, N, P, B, n, maxit, flags)
     if record:
         workspace = Workspace()
@@ -474,7 +483,8 @@ def tvd_fft_multi(y, lams, rhos, maxit=100, *, out=None, record=False, need_rho=
     if not record:
         return out
     rec = MultiRecording()
-    rec.workspace, rec.dims, rec.maxit, rec.masks, rec.dv = workspace, (M, N, P, B, n), int(maxit), not need_rho, dv
+    rec.workspace, rec.dims, rec.maxit, rec.masks, rec.dv = (workspace, (M, N, P, B, n), int(maxit),
+                                                             not need_rho or isotropic, dv)
     return out, rec
 
 
@@ -504,11 +514,13 @@ class _TvdFFTMultiFn(torch.autograd.Function):
     """Differentiable tvd_fft_multi: one recorded forward of every branch, one reverse sweep."""
 
     @staticmethod
-    def forward(ctx, y, maxit, n, *params):
+    def forward(ctx, y, maxit, iso, n, *params):
         lams, rhos = params[:n], params[n:]
         ctx.n = n
-        need_rho = any(ctx.needs_input_grad[3 + n + i] for i in range(n))
-        x, ctx.rec = tvd_fft_multi(y, lams, rhos, maxit, record=True, need_rho=need_rho)
+        need_rho = any(ctx.needs_input_grad[4 + n + i] for i in range(n))
+        if iso and need_rho:
+            raise NotImplementedError("rho_bar of the isotropic multi-branch solve: solve the branches one by one")
+        x, ctx.rec = tvd_fft_multi(y, lams, rhos, maxit, record=True, need_rho=need_rho, isotropic=iso)
         ctx.need_rho = need_rho
         ctx.save_for_backward(y, x, *params)
         return x
@@ -520,21 +532,22 @@ class _TvdFFTMultiFn(torch.autograd.Function):
         yb, lb, rb = tvd_fft_multi_backward_recorded(ctx.rec, x, x_bar, need_y=ctx.needs_input_grad[0],
                                                      need_rho=ctx.need_rho)
         ctx.rec = None
-        grads = [yb if ctx.needs_input_grad[0] else None, None, None]
+        grads = [yb if ctx.needs_input_grad[0] else None, None, None, None]
         for i in range(n):
             p = params[i]
-            grads.append(lb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[3 + i] else None)
+            grads.append(lb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[4 + i] else None)
         for i in range(n):
             p = params[n + i]
-            grads.append(rb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[3 + n + i] else None)
+            grads.append(rb[i:i + 1].reshape(p.shape).to(p.dtype) if ctx.needs_input_grad[4 + n + i] else None)
         return tuple(grads)
 
 
-def tvd_fft_multi_grad(y, lams, rhos, maxit=100):
+def tvd_fft_multi_grad(y, lams, rhos, maxit=100, isotropic=False):
     """tvd_fft_multi under autograd when y or any lam / rho tensor requires grad (else the plain call)."""
     ts = [t for t in (y, *lams, *rhos) if isinstance(t, torch.Tensor)]
     if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
         dev = y.device
         as_t = lambda v: v if isinstance(v, torch.Tensor) else torch.full((1,), float(v), device=dev)  # noqa: E731
-        return _TvdFFTMultiFn.apply(y, int(maxit), len(lams), *[as_t(v) for v in lams], *[as_t(v) for v in rhos])
-    return tvd_fft_multi(y, lams, rhos, maxit)
+        return _TvdFFTMultiFn.apply(y, int(maxit), bool(isotropic), len(lams), *[as_t(v) for v in lams],
+                                    *[as_t(v) for v in rhos])
+    return tvd_fft_multi(y, lams, rhos, maxit, isotropic=isotropic)

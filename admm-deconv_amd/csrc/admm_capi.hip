@@ -1301,10 +1301,14 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
 // slots hold each branch's Vsum (natural layout, y_bar only) and the s slots D x_K (rho_bar only).
 struct MultiLayout {
     size_t prm, twM, twN, C, F, hln, sln, traj, sbar, vsl, part, rt, rtmp, total;
+    size_t fmap, qpart, nrm, rmap;   // isotropic (ADMM_MULTI_ISO): f maps, q / R partials, |s| slots, R maps
 };
 constexpr int kMultiM = 256, kMultiN = 256;
 size_t multi_C_bytes() { return align_up((size_t)(kMultiM / 2 + 1) * kMultiN * 4); }
 size_t multi_F_bytes() { return align_up(admm::plane::tables_bytes()); }
+
+// tau_bar partial rows of one branch's isotropic sweep: 512 per reverse step k = K .. 2 (iso_radj_kernel)
+size_t multi_iso_rows(int K) { return (size_t)(K > 1 ? K - 1 : 1) * 512; }
 
 MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
     MultiLayout L{};
@@ -1316,7 +1320,8 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
     };
     const size_t MN = (size_t)kMultiM * kMultiN;
     const int K = maxit < 1 ? 1 : maxit;
-    const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = (flags & ADMM_REC_MASKS) != 0;
+    const bool rec = (flags & ADMM_MULTI_RECORD) != 0, iso = (flags & ADMM_MULTI_ISO) != 0;
+    const bool masks = (flags & ADMM_REC_MASKS) != 0 && !iso;
     L.prm = take((size_t)nbr * 16);
     L.twM = take(kMultiM * 8);
     L.twN = take(kMultiN * 8);
@@ -1328,9 +1333,17 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
         L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 2 : MN * 8));
         L.sbar = take(planes * MN * 8);
         L.vsl = take(planes * MN * 4);
-        L.part = take(planes * 16);
+        L.part = take(iso ? (size_t)nbr * multi_iso_rows(K) * 16 : planes * 16);
         L.rt = take((size_t)nbr * 16);
         L.rtmp = take((size_t)kRedParts * 2 * 8);
+    }
+    if (iso) {
+        L.fmap = take((size_t)nbr * MN * 4);
+        L.qpart = take(planes * MN * 4);
+        if (rec) {
+            L.nrm = take((size_t)(K > 1 ? K - 1 : 1) * nbr * MN * 4);
+            L.rmap = take((size_t)nbr * MN * 4);
+        }
     }
     L.total = off;
     return L;
@@ -1339,10 +1352,12 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
 int check_multi(int M, int N, int P, int B, int nbr, int maxit, int flags) {
     if (P < 1 || B < 1 || nbr < 1) return fail(ADMM_E_INVALID, "sizes must be positive (P=%d B=%d nbranch=%d)", P, B, nbr);
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0 (got %d)", maxit);
-    if (flags & ~(ADMM_MULTI_RECORD | ADMM_REC_MASKS)) return fail(ADMM_E_INVALID, "unknown flags 0x%x", flags);
+    if (flags & ~(ADMM_MULTI_RECORD | ADMM_REC_MASKS | ADMM_MULTI_ISO)) return fail(ADMM_E_INVALID, "unknown flags 0x%x", flags);
     if (M != kMultiM || N != kMultiN || !fused_enabled())
-        return fail(ADMM_E_UNSUPPORTED, "the multi-branch solve is the fused 256 x 256 anisotropic kernel (got %d x %d%s); "
+        return fail(ADMM_E_UNSUPPORTED, "the multi-branch solve is the fused 256 x 256 kernels (got %d x %d%s); "
                                         "solve the branches one by one", M, N, fused_enabled() ? "" : ", option FUSED = 0");
+    if ((flags & ADMM_MULTI_ISO) && (flags & ADMM_MULTI_RECORD) && !fused_adj_enabled())
+        return fail(ADMM_E_UNSUPPORTED, "an isotropic multi-branch recording needs the fused reverse sweep (option FUSED_ADJ)");
     if ((size_t)P * B * nbr > kChunkPlanes)
         return fail(ADMM_E_UNSUPPORTED, "at most %zu planes (nbranch * P * B) per multi-branch call", kChunkPlanes);
     return ADMM_OK;
@@ -1369,9 +1384,10 @@ int forward_multi(const float* y, float* x_out, int M, int N, int P, int B, int 
         std::lock_guard<std::mutex> lk(g_rec_mu);
         g_rec.erase(workspace);
         if (flags & ADMM_MULTI_RECORD) {
-            RecTag t = make_tag(M, N, P, B, 0, 0, 0, maxit, false, admm::ScalarSrc{lambda[0], rho[0], 0.f, 0.f});
+            const int iso = (flags & ADMM_MULTI_ISO) != 0;
+            RecTag t = make_tag(M, N, P, B, 0, 0, iso, maxit, false, admm::ScalarSrc{lambda[0], rho[0], 0.f, 0.f});
             t.nbr = nbr;
-            t.masks = (flags & ADMM_REC_MASKS) != 0;
+            t.masks = (flags & ADMM_REC_MASKS) != 0 || iso;   // no rho_bar from either
             g_rec[workspace] = t;
         }
     }
@@ -1403,6 +1419,30 @@ int forward_multi(const float* y, float* x_out, int M, int N, int P, int B, int 
     }
     const admm::plane::Branches br = multi_branches(P, B, nbr);
     const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = rec && (flags & ADMM_REC_MASKS) != 0;
+    if (flags & ADMM_MULTI_ISO) {
+        // isotropic: per iteration one plane256_iso_kernel over every branch's planes and one iso_norm_kernel
+        // (each branch's batch norm over its own planes); recording: s_{k+1} into slot k, |s_{k+1}| too
+        namespace pk = admm::plane;
+        const size_t kE = (size_t)M * N / 2;
+        float4* st = reinterpret_cast<float4*>(ws + (rec ? L.traj : L.sln));
+        const size_t tslot = rec ? planes * kE : 0;
+        float2* fl = reinterpret_cast<float2*>(ws + L.fmap);
+        float2* ql = reinterpret_cast<float2*>(ws + L.qpart);
+        for (int k = 0; k < maxit; ++k) {
+            rc = ln.run(ADMM_K_PLANE, [&] {
+                return pk::launch_plane_iso(y, x_out, ws + L.F, false, reinterpret_cast<float2*>(ws + L.hln),
+                                            st + (k > 0 ? (size_t)(k - 1) * tslot : 0), st + (size_t)k * tslot, fl, ql,
+                                            prm, k, maxit, planes, s, &br);
+            });
+            if (rc) return rc;
+            if (k + 1 < maxit) {
+                float2* nr = rec ? reinterpret_cast<float2*>(ws + L.nrm) + (size_t)k * nbr * kE : nullptr;
+                rc = ln.run(ADMM_K_NORM, [&] { return pk::launch_iso_norm(ql, fl, nr, prm, planes, s, &br); });
+                if (rc) return rc;
+            }
+        }
+        return ln.finish();
+    }
     rc = ln.run(ADMM_K_PLANE, [&] {
         return admm::plane::launch_plane(y, x_out, ws + L.F, false, reinterpret_cast<float2*>(ws + L.hln),
                                          reinterpret_cast<float4*>(ws + L.sln), prm, maxit, planes, s,
@@ -1428,15 +1468,17 @@ int backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, float* r
         if (it == g_rec.end() || it->second.nbr != nbr)
             return fail(ADMM_E_INVALID, "workspace holds no multi-branch recording of %d branches "
                                         "(admm_tvd_forward_multi_dev_f32 with ADMM_MULTI_RECORD first)", nbr);
-        RecTag t = make_tag(M, N, P, B, 0, 0, 0, maxit, false, admm::ScalarSrc{&g_dummy_scalar, &g_dummy_scalar, 0.f, 0.f});
+        const int iso = it->second.iso;
+        RecTag t = make_tag(M, N, P, B, 0, 0, iso, maxit, false, admm::ScalarSrc{&g_dummy_scalar, &g_dummy_scalar, 0.f, 0.f});
         t.nbr = nbr;
         t.masks = it->second.masks;
+        if (iso) flags |= ADMM_MULTI_ISO;
         if (!(it->second == t))
             return fail(ADMM_E_INVALID, "replay does not match its multi-branch recording (shape, maxit or library "
                                         "options changed)");
         if (t.masks && rho_bar)
-            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only): rho_bar cannot be "
-                                        "formed from it");
+            return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only) or ADMM_MULTI_ISO: "
+                                        "rho_bar cannot be formed from it");
         if (t.masks) flags |= ADMM_REC_MASKS;
         g_rec.erase(it);
     }
@@ -1458,6 +1500,57 @@ int backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, float* r
     const admm::plane::Branches br = multi_branches(P, B, nbr);
     const float* prm = reinterpret_cast<const float*>(ws + L.prm);
     const bool masks = (flags & ADMM_REC_MASKS) != 0;
+    if (flags & ADMM_MULTI_ISO) {
+        // isotropic fused sweep over every branch's planes (plane_iso.hip): per reverse step one
+        // plane256_isoadj_kernel and one iso_radj_kernel; vbar in the forward's dead s state, Vsum lane-native
+        // in vsl and natural (per grid plane) in the H^T y slots, R partials in the q partial slots
+        namespace pk = admm::plane;
+        const size_t kE = MN / 2, rows = multi_iso_rows(K);
+        float4* trs = reinterpret_cast<float4*>(ws + L.traj);
+        const float2* trn = reinterpret_cast<const float2*>(ws + L.nrm);
+        float2* vb = reinterpret_cast<float2*>(ws + L.sln);
+        float2* rmap = reinterpret_cast<float2*>(ws + L.rmap);
+        float2* rpl = reinterpret_cast<float2*>(ws + L.qpart);
+        float* vout = y_bar ? reinterpret_cast<float*>(ws + L.hln) : nullptr;
+        double* part = reinterpret_cast<double*>(ws + L.part);
+        if ((e = hipMemsetAsync(part, 0, (size_t)nbr * rows * 16, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
+        for (int k = K; k >= 1; --k) {
+            rc = ln.run(ADMM_K_ADJ, [&] {
+                return pk::launch_plane_isoadj(x_bar, ws + L.F, trs, planes * kE, trn, nbr * kE, vb,
+                                               reinterpret_cast<float4*>(ws + L.sbar), rmap, rpl,
+                                               reinterpret_cast<float2*>(ws + L.vsl), vout, prm, k, K, planes, s, &br);
+            });
+            if (rc) return rc;
+            if (k >= 2) {
+                rc = ln.run(ADMM_K_NORM, [&] {
+                    return pk::launch_iso_radj(rpl, rmap, trn + (size_t)(k - 2) * nbr * kE,
+                                               part + (size_t)(K - k) * 512 * 2, rows * 2, prm, planes, s, &br);
+                });
+                if (rc) return rc;
+            }
+        }
+        double* rt = reinterpret_cast<double*>(ws + L.rt);
+        for (int i = 0; i < nbr; ++i) {
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                launch_reduce_cols(s, part + (size_t)i * rows * 2, rt + 2 * i, (int)rows, 2,
+                                   reinterpret_cast<double*>(ws + L.rtmp));
+            });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(admm::grads_final_kernel, dim3(1), dim3(64), 0, s, rt + 2 * i, (const double*)nullptr,
+                                   (const double*)nullptr, 0, prm + 4 * i, lambda_bar ? lambda_bar + i : nullptr,
+                                   (float*)nullptr, (float*)nullptr);
+            });
+            if (rc) return rc;
+        }
+        if (y_bar) {
+            rc = ln.run(ADMM_K_FINAL, [&] {
+                hipLaunchKernelGGL(admm::branch_sum_kernel, dim3(1024), dim3(kThreads), 0, s, vout, y_bar, ppb * MN, nbr);
+            });
+            if (rc) return rc;
+        }
+        return ln.finish();
+    }
     float4* dxK = rho_bar ? reinterpret_cast<float4*>(ws + L.sln) : nullptr;   // the forward's s state is dead
     float* vbuf = y_bar ? reinterpret_cast<float*>(ws + L.hln) : nullptr;     // ... and its H^T y copies
     double* part = reinterpret_cast<double*>(ws + L.part);

@@ -95,6 +95,8 @@ def parse():
                     help="c5: run the Parallel branches one after the other on one stream (the reference's order)")
     ap.add_argument("--no-merge", action="store_true",
                     help="c5: solve the Parallel branches one by one (per-branch streams) instead of one grid")
+    ap.add_argument("--merge-iso", action="store_true",
+                    help="c5 --iso: the branches in one grid (ADMM_MULTI_ISO) instead of one stream each")
     ap.add_argument("--iso", action="store_true",
                     help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
     return ap.parse_args()
@@ -148,7 +150,7 @@ def bench_c5(args, dev):
     target = torch.from_numpy(np.concatenate([clean] * reps)[:B]).to(dev).repeat(1, len(branch), 1, 1)
 
     net = layers.Parallel(layers.chcat, *branch, streams=not args.serial_branches,   # net_build.jl:121-125
-                          merge=not (args.no_merge or args.serial_branches))
+                          merge=False if (args.no_merge or args.serial_branches) else ("always" if args.merge_iso else True))
     merged = net._mergeable(x)
 
     def step():
@@ -184,7 +186,24 @@ def bench_c5(args, dev):
             kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
     roof = None
     planes = B * P
-    if merged:
+    if merged and args.iso:
+        # one grid of 5 x 192 planes per iteration / reverse step (plane_iso.hip, ADMM_MULTI_ISO)
+        fwd, adj = iso_fused_bytes_per_px(K)
+        nb = len(branch)
+        per = {"plane": nb * planes * M * N * fwd / K, "adjoint": nb * planes * M * N * adj / K}
+        for k, b in per.items():
+            if k in kernels:
+                kernels[k]["algorithmic_bytes_per_launch"] = b
+                kernels[k]["achieved_GBps"] = round(b / (kernels[k]["avg_ms"] * 1e-3) / 1e9, 1)
+        dom = max((k for k in per if k in kernels), key=lambda k: kernels[k]["total_ms_per_step"])
+        a = kernels[dom]
+        ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": f"{dom} (plane_iso.hip, one grid of {nb} branches x {planes} planes, "
+                                          f"{K} launches)", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic("c5isom", dom), "algorithmic_bytes_per_launch": per[dom],
+                "avg_launch_ms": round(a["avg_ms"], 5)}
+    elif merged:
         # one grid of 5 x 192 planes for the forward (plane256_kernel recording ST mask bits: lambda is the
         # only trainable, rho_bar is not formed) and one for the reverse sweep (plane256_adj_kernel<masks>).
         # Per pixel: forward y in, H^T y copy out (4 + 4), per iteration H^T y in (4, K-1 times), s in / out

@@ -149,8 +149,10 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
  *       iteration) instead of s_k itself: 16x less trajectory memory and, in the fused
  *       256 x 256 anisotropic reverse sweep, 8 of its 24 B/px per step gone.  lambda_bar, y_bar and h_bar
  *       are bitwise those of a full recording; a replay with rho_bar != NULL fails with ADMM_E_INVALID.
- *       Honoured by the fused anisotropic trajectory (256 x 256, no h_bar); elsewhere the full
- *       trajectory is recorded and rho_bar stays available. */
+ *       Honoured by the fused anisotropic trajectory (256 x 256, no h_bar); isotropic at 256 x 256 (no
+ *       h_bar, no reducer) it selects the fused isotropic sweep instead (plane_iso.hip: s_k and |s_k| kept
+ *       in the kernels' lane-native layout, no rho_bar either); elsewhere the full trajectory is recorded
+ *       and rho_bar stays available. */
 enum { ADMM_REC_HBAR = 1, ADMM_REC_MASKS = 2 };
 
 int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B,
@@ -199,15 +201,17 @@ int admm_tvd_backward_recorded_dev_f32(const float* y, const float* x_bar, float
  * pointers) and writes the chcat layout: x_out is Julia (M, N, nbranch*P, B) == C
  * `float[B][nbranch*P][N][M]`, branch i's channels at i*P .. i*P+P-1 -- the output of
  * `Parallel(chcat, ...)` itself, before the layers' bias / σ.  All nbranch*P*B planes run in one grid of
- * the fused kernel, so no CU idles between branches.  Anisotropic, 256 x 256, no PSF, at most 65,280
+ * the fused kernel, so no CU idles between branches.  256 x 256, no PSF, at most 65,280
  * planes in total (nbranch*P*B); the same results, bitwise, as nbranch separate solves.
  * flags: ADMM_MULTI_RECORD (1) records the trajectory for admm_tvd_backward_multi_recorded_dev_f32
- *        (the workspace then holds it until the replay); | ADMM_REC_MASKS (2) as above (no rho_bar).
+ *        (the workspace then holds it until the replay); | ADMM_REC_MASKS (2) as above (no rho_bar);
+ *        | ADMM_MULTI_ISO (4): isotropic prox (use_iso) -- the split-iteration kernels of plane_iso.hip,
+ *        each branch's batch norm over its own planes; its recording never gives rho_bar.
  * The backward writes lambda_bar[i] (and rho_bar[i]; device arrays of nbranch floats, NULL = not
  * needed; rho_bar must be NULL with ADMM_REC_MASKS) and y_bar = the sum over branches of each branch's
  * input gradient (NULL = not needed, cheaper), from x_bar in the chcat layout of x_out.  x_out must
  * still hold the recorded output. */
-enum { ADMM_MULTI_RECORD = 1 };
+enum { ADMM_MULTI_RECORD = 1, ADMM_MULTI_ISO = 4 };
 int admm_tvd_multi_workspace_bytes(int M, int N, int P, int B, int nbranch, int maxit, int flags,
                                    size_t* out_bytes);
 int admm_tvd_forward_multi_dev_f32(const float* y, float* x_out, int M, int N, int P, int B, int nbranch,

@@ -66,24 +66,25 @@ def test_creg_clamp(dev):
     assert abs(L.lam.item() - 0.01) < 1e-7 and abs(L.rho.item() - 0.01) < 1e-7
 
 
+@pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])
 @pytest.mark.parametrize("train_rho", [False, True], ids=["lam", "lam+rho"])
-def test_parallel_branches_on_streams_match_serial(dev, train_rho):
+def test_parallel_branches_on_streams_match_serial(dev, train_rho, iso):
     """Parallel(chcat, ...) (net_build.jl:121-125): the branches in ONE grid (the default for ADMM branches
     the fused kernel covers), each branch on its own HIP stream, and the branches run one after the other
     give the same forward output and the same parameter gradients, bitwise; the input gradient (a sum over
     the branches, added in a different order) to fp32 rounding.  train_rho: rho trainable too, so the
-    recordings keep the full trajectory instead of the ST mask bits."""
+    recordings keep the full trajectory instead of the ST mask bits (isotropic: no one-grid solve then)."""
     from admm_deconv import layers
     x0 = torch.from_numpy(synth.make_batch(3, 256, 256, None, P=3, sigma=0.1)).to(dev)
     grads = []
-    for streams, merge in ((True, False), (False, False), (True, True)):
+    for streams, merge in ((True, False), (False, False), (True, "always")):
         rng = np.random.default_rng(5)
-        branch = [layers.ADMMDeconvF2((), 12, r, layers.relu1, rng=rng, device=dev) for r in (0.002, 0.2, 4.0)]
+        branch = [layers.ADMMDeconvF2((), 12, r, layers.relu1, iso=iso, rng=rng, device=dev) for r in (0.002, 0.2, 4.0)]
         for L in branch:
             L.lam.requires_grad_(True)
             L.rho.requires_grad_(train_rho)
         net = layers.Parallel(layers.chcat, *branch, streams=streams, merge=merge)
-        assert net._mergeable(x0) == merge
+        assert net._mergeable(x0) == (bool(merge) and not (iso and train_rho))
         x = x0.clone().requires_grad_(True)
         out = net(x)
         (out * torch.linspace(0, 1, out.shape[1], device=dev).reshape(1, -1, 1, 1)).sum().backward()

@@ -2,7 +2,8 @@
 -- the branches of Parallel(chcat, ADMMDeconvF2((), K, rho_i, relu1) ...) of src/nets/net_build.jl:113-125 in
 one launch of the fused kernel -- against the same branches solved one by one through the single-solve
 ABI: forward bitwise (chcat layout), lambda_bar / rho_bar bitwise, y_bar (a sum over branches) to fp32
-rounding; and the mask-bit trajectory (ADMM_REC_MASKS) against the full one."""
+rounding; the mask-bit trajectory (ADMM_REC_MASKS) against the full one; and the isotropic one-grid solve
+(ADMM_MULTI_ISO, plane_iso.hip: each branch's batch norm over its own planes) the same way."""
 import numpy as np
 import pytest
 import torch
@@ -126,3 +127,48 @@ def test_multi_deterministic(dev):
         outs.append((x,) + admm_deconv.tvd_fft_multi_backward_recorded(rec, x, xb, need_rho=False)[:2])
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(*outs))
+
+
+@pytest.mark.parametrize("n,B,P,K", [(5, 2, 3, 12), (2, 1, 1, 1), (3, 3, 1, 2)])
+def test_multi_iso_is_the_branches(dev, n, B, P, K):
+    """Isotropic: forward bitwise the single fused solves; lambda_bar bitwise the single fused sweeps; y_bar
+    their sum to rounding."""
+    y = torch.from_numpy(synth.make_batch(B, 256, 256, None, P=P, sigma=0.1, g0=4)).to(dev)
+    lams, rhos = _branch_scalars(dev, n, seed=11)
+    xp = admm_deconv.tvd_fft_multi(y, lams, rhos, K, isotropic=True)
+    xb = torch.randn((B, n * P, 256, 256), device=dev)
+    x, rec = admm_deconv.tvd_fft_multi(y, lams, rhos, K, record=True, need_rho=False, isotropic=True)
+    yb, lb, rb = admm_deconv.tvd_fft_multi_backward_recorded(rec, x, xb, need_rho=False)
+    yb_sum = torch.zeros_like(y)
+    for i in range(n):
+        xi, reci = admm_deconv.tvd_fft_record(y, lams[i], rhos[i], None, True, K, need_rho=False)
+        ybi, _, lbi, _ = admm_deconv.tvd_fft_backward_recorded(reci, xi, xb[:, i * P:(i + 1) * P].contiguous(),
+                                                               need_rho=False)
+        torch.cuda.synchronize()
+        assert torch.equal(xi, x[:, i * P:(i + 1) * P]), i
+        assert torch.equal(lbi.reshape(1), lb[i:i + 1]), (i, float(lbi), float(lb[i]))
+        yb_sum += ybi
+    torch.cuda.synchronize()
+    assert rb is None and torch.equal(x, xp)
+    assert torch.allclose(yb, yb_sum, rtol=1e-6, atol=1e-6 * float(yb_sum.abs().max()))
+
+
+def test_multi_iso_vs_oracle_and_refusals(dev):
+    y = synth.make_batch(2, 256, 256, None, P=3, sigma=0.1, g0=8)
+    lams, rhos = _branch_scalars(dev, 3, seed=2)
+    x = admm_deconv.tvd_fft_multi(torch.from_numpy(y).to(dev), lams, rhos, 15, isotropic=True).cpu().numpy()
+    for i in (0, 2):
+        ref = oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)),
+                                         torch.tensor(float(lams[i]), dtype=torch.float64),
+                                         torch.tensor(float(rhos[i]), dtype=torch.float64), None, True, 15).numpy()
+        assert_parity(x[:, 3 * i:3 * i + 3], ref, what=f"iso branch {i}")
+    yt = torch.from_numpy(y).to(dev)
+    with pytest.raises(ValueError):
+        admm_deconv.tvd_fft_multi(yt, lams, rhos, 5, record=True, need_rho=True, isotropic=True)
+    # the C-ABI refuses rho_bar from an isotropic recording
+    x, rec = admm_deconv.tvd_fft_multi(yt, lams, rhos, 5, record=True, need_rho=False, isotropic=True)
+    scal = torch.zeros(6, device=dev)
+    ws_ptr, ws_len = rec.workspace.get(0, dev, None)
+    rc = _lib.load().admm_tvd_backward_multi_recorded_dev_f32(x.data_ptr(), None, scal.data_ptr(), scal.data_ptr() + 12,
+                                                              256, 256, 3, 2, 3, 5, x.data_ptr(), ws_ptr, ws_len, None)
+    assert rc == _lib.ADMM_E_INVALID

@@ -18,6 +18,14 @@ CLASS = {"line_kernel": "line", "column_kernel<256, false>": "column", "iso_a_ke
 
 
 def klass(name):
+    if "plane256_isoadj_kernel" in name:
+        return "adjoint"
+    if "plane256_iso_kernel" in name:
+        return "plane"
+    if "iso_norm_kernel" in name:
+        return "norm"
+    if "iso_radj_kernel" in name:
+        return "radj"
     if "plane256_kernel" in name:
         return "plane"
     if "plane256_adj_kernel" in name:
