@@ -140,7 +140,12 @@ __device__ __forceinline__ void fft64_reg_stage(float2 (&x)[64], float2* stg, fl
 template <int K>
 __device__ __forceinline__ void combine_fwd(float2 (&x)[64], bool hb) {
     if constexpr (K < 64) {
-        const float2 mine = hb ? w256<2 * K, false>(x[K]) : x[K];
+        float2 xk = x[K];
+        // K = 32: W256^64 = -i is a swap of the fields, and `hb ? (y, -x) : (x, y)` on a register still in
+        // the front end's S array becomes a select of field ADDRESSES -- S[32] then stays in scratch (the PSF
+        // kernel: every access to it a scratch load / store).  The pin makes it a select of values.
+        if constexpr (2 * K == 64) __asm__ volatile("" : "+v"(xk.x), "+v"(xk.y));
+        const float2 mine = hb ? w256<2 * K, false>(xk) : xk;
         const float2 oth = swap_pair(mine);
         x[K] = hb ? csub(oth, mine) : cadd(mine, oth);
         if constexpr ((K & 15) == 15) sched_fence();
