@@ -22,6 +22,11 @@
 namespace admm {
 namespace plane {
 
+// registers of s / map loads in flight ahead of the one being processed in the iso row phases
+#ifndef ISO_PD
+#define ISO_PD 2
+#endif
+
 
 // BT factor f = max(1 - tau/n, 0) from r = rcp(n) (v_rcp_f32: one rounding off the quotient, the same
 // expression in the forward's iso_norm_kernel and the reverse sweep, so the sweep re-forms f bit for bit;
@@ -36,7 +41,7 @@ __device__ __forceinline__ float bt_f(float tau, float r) {
 // q = (s1^2 + s2^2 of the lane's two pixels) to qst.  Neighbours as in row_update.
 __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t sst, rsrc_t fld, rsrc_t qst, float2* xb,
                                           float2* colbuf, int t, bool hb, bool first) {
-    constexpr int PD = 2, NR = PD + 1;
+    constexpr int PD = ISO_PD, NR = PD + 1;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
     float2* stg = colbuf + t;
@@ -98,7 +103,7 @@ __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t ss
 // through the wb buffer after the barrier).
 __device__ __forceinline__ void row_iso_b(float2 (&S)[64], rsrc_t sld, rsrc_t fld, rsrc_t hp, float2* wb, float2* sink,
                                           int t, bool hb, float rho) {
-    constexpr int PD = 2, NR = PD + 1;
+    constexpr int PD = ISO_PD, NR = PD + 1;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
     float4 sr[NR];
@@ -290,7 +295,7 @@ template <bool WV>
 __device__ __forceinline__ void row_isoadj_a(float2 (&S)[64], rsrc_t vst, rsrc_t vlr, rsrc_t vsr, unsigned vso,
                                              unsigned vss, rsrc_t s1p, rsrc_t sbl, rsrc_t rst, float2* xb, float2* colbuf,
                                              int t, bool hb, float rho) {
-    constexpr int PD = 2, NR = PD + 1;
+    constexpr int PD = ISO_PD, NR = PD + 1;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
     float2* stg = colbuf + t;
@@ -359,7 +364,7 @@ __device__ __forceinline__ void row_isoadj_a(float2 (&S)[64], rsrc_t vst, rsrc_t
 __device__ __forceinline__ void row_isoadj_b(float2 (&S)[64], rsrc_t s1p, rsrc_t sbl, rsrc_t sbs, rsrc_t rp, rsrc_t np,
                                              float2* xb, float2* wb, float2* sink, float2* colbuf, int t, bool hb,
                                              float tau, float rho) {
-    constexpr int PD = 2, NR = PD + 1;
+    constexpr int PD = ISO_PD, NR = PD + 1;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
     float2* stg = colbuf + t;
