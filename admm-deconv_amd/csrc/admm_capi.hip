@@ -465,7 +465,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         });
         return rc;
     }
-    if (iso && fused_tables_shape(M, N) && !red && (!tr.s || tr.iso_lane) && !tr.v && fused_enabled()) {
+    if (iso && fused_tables_shape(M, N) && (!tr.s || tr.iso_lane) && !tr.v && fused_enabled()) {
         // isotropic at 256 x 256: the split-iteration per-plane kernels (plane_iso.hip), the spectrum
         // resident in the CU; per iteration one plane256_iso_kernel and one iso_norm_kernel (batch norm)
         namespace pk = admm::plane;
@@ -485,7 +485,19 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
             if (rc) return rc;
             if (k + 1 < maxit) {
                 float2* nr = tr.iso_lane ? reinterpret_cast<float2*>(tr.nrm + (size_t)k * MN) : nullptr;
-                rc = ln.run(ADMM_K_NORM, [&] { return pk::launch_iso_norm(ql, fl, nr, prm, planes, s); });
+                if (red) {
+                    // sharded batch: this shard's sums, the caller's all-reduce of the M x N map, then f
+                    float2* sm = reinterpret_cast<float2*>(ws + lay.part);
+                    rc = ln.run(ADMM_K_NORM, [&] { return pk::launch_iso_norm(ql, fl, nr, prm, planes, s, nullptr, sm); });
+                    if (rc) return rc;
+                    rc = call_reducer(red, reinterpret_cast<float*>(sm), MN, s);
+                    if (rc) return rc;
+                    rc = ln.run(ADMM_K_NORM, [&] {
+                        return pk::launch_iso_norm(ql, fl, nr, prm, planes, s, nullptr, nullptr, sm);
+                    });
+                } else {
+                    rc = ln.run(ADMM_K_NORM, [&] { return pk::launch_iso_norm(ql, fl, nr, prm, planes, s); });
+                }
                 if (rc) return rc;
             }
         }
@@ -958,7 +970,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     // and taken by the combined call whenever rho_bar is not wanted
     // isotropic at 256 x 256: the split-iteration fused forward records s and |s| lane-native for the fused
     // reverse sweep (plane_iso.hip) -- also without rho_bar, so the same flag selects it
-    const bool iso_ok = iso && fused_tables_shape(M, N) && !red && !want_h && fused_enabled() && fused_adj_enabled();
+    const bool iso_ok = iso && fused_tables_shape(M, N) && !want_h && fused_enabled() && fused_adj_enabled();
     const bool masks_ok = (ln_traj && !iso && fused_adj_enabled()) || iso_ok;
     bool use_masks = masks_ok && (phases == 1 ? (rec_flags & ADMM_REC_MASKS) != 0 : rho_bar == nullptr);
     if (phases == 2) {
@@ -1097,6 +1109,12 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
                                                prm, planes, s);
                 });
                 if (rc) return rc;
+                // sharded batch: tau_bar above used this shard's R (shard contributions add up); sbar needs the
+                // whole batch's R
+                if (red) {
+                    rc = call_reducer(red, reinterpret_cast<float*>(rmap), MN, s);
+                    if (rc) return rc;
+                }
             }
         }
         red_rows = (K > 1 ? K - 1 : 1) * 512;

@@ -63,13 +63,15 @@ hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* t
 // Isotropic (BT) solve at 256 x 256 (plane_iso.hip): iteration k = 0 .. K-1 of every plane (hln: H^T y,
 // lane-native, written at k = 0; s_in / s_out: s_k / s_{k+1}, the same state buffer, or trajectory slots k-1 / k
 // when recording; fmap: the branch's lane-native BT factor f_k, k > 0; qpart: per plane |s_{k+1}|^2 partials),
-// then, between iterations, launch_iso_norm (f_{k+1} and, when nrm is given, |s_{k+1}|, per branch from qpart).
+// then, between iterations, launch_iso_norm (f_{k+1} and, when nrm is given, |s_{k+1}|, per branch from qpart;
+// a sharded batch: sum_out = this shard's sums only, then, after the caller's all-reduce, sum_in = the sums).
 // One plane's maps are 64 x 512 float2.
 hipError_t launch_plane_iso(const float* y, float* x_out, const void* tables, bool psf, float2* hln, const float4* s_in,
                             float4* s_out, const float2* fmap, float2* qpart, const float* prm, int k, int K,
                             size_t planes, hipStream_t s, const Branches* br = nullptr);
 hipError_t launch_iso_norm(const float2* qpart, float2* fmap, float2* nrm, const float* prm, size_t planes,
-                           hipStream_t s, const Branches* br = nullptr);
+                           hipStream_t s, const Branches* br = nullptr, float2* sum_out = nullptr,
+                           const float2* sum_in = nullptr);
 // Reverse step k = K .. 1 of the isotropic solve on that recording (traj: s_1..s_{K-1}, slot stride tslot
 // float4; nrm: |s_1|..|s_{K-1}|, slot stride nslot float2), no rho_bar; vbuf / sbar / Rmap / rpart / vsl:
 // lane-native vbar_k, sbar_k, R map (per branch), R partials (per plane), Vsum; vout: Vsum in the natural

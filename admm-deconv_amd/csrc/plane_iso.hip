@@ -244,26 +244,40 @@ __global__ __launch_bounds__(kPT) void plane256_iso_kernel(const float* __restri
 // |s|^2 of every pixel summed over one branch's planes (fixed order: slice j of 4 adds planes j, j+4, ...,
 // the slices then in order: deterministic), f = max(1 - tau/|s|, 0) (ops.jl:10; NaN kept as the
 // reference's 0/0 gives it).  grid (64 * 512 / 64, nbr) x 256: 64 lane-native float2 elements per block.
+// Sharded batch (admm_batch_reducer): sum_out != NULL writes this shard's sums there and stops; after the
+// caller's all-reduce of that map, sum_in != NULL takes the sums from it instead of the planes.
 __global__ __launch_bounds__(256) void iso_norm_kernel(const float2* __restrict__ qpart, float2* __restrict__ fmap,
                                                        float2* __restrict__ nrm_out, const float* __restrict__ prm,
-                                                       Branches br) {
+                                                       Branches br, float2* __restrict__ sum_out,
+                                                       const float2* __restrict__ sum_in) {
     __shared__ float2 red[256];
     const int i = blockIdx.y;
     const int e = blockIdx.x * 64 + (threadIdx.x & 63), slice = threadIdx.x >> 6;
     constexpr size_t kE = 64 * kPT;   // float2 elements per plane
-    const float2* q = qpart + (size_t)i * br.ppb * kE + e;
-    float2 a = make_float2(0.f, 0.f);
+    float sx, sy;
+    if (sum_in) {
+        if (slice) return;
+        const float2 v = sum_in[(size_t)i * kE + e];
+        sx = v.x, sy = v.y;
+    } else {
+        const float2* q = qpart + (size_t)i * br.ppb * kE + e;
+        float2 a = make_float2(0.f, 0.f);
 #pragma unroll 4
-    for (int p = slice; p < br.ppb; p += 4) {
-        const float2 v = q[(size_t)p * kE];
-        a.x += v.x;
-        a.y += v.y;
+        for (int p = slice; p < br.ppb; p += 4) {
+            const float2 v = q[(size_t)p * kE];
+            a.x += v.x;
+            a.y += v.y;
+        }
+        red[threadIdx.x] = a;
+        __syncthreads();
+        if (slice) return;
+        const float2 b = red[64 + threadIdx.x], c = red[128 + threadIdx.x], d = red[192 + threadIdx.x];
+        sx = ((a.x + b.x) + c.x) + d.x, sy = ((a.y + b.y) + c.y) + d.y;
+        if (sum_out) {
+            sum_out[(size_t)i * kE + e] = make_float2(sx, sy);
+            return;
+        }
     }
-    red[threadIdx.x] = a;
-    __syncthreads();
-    if (slice) return;
-    const float2 b = red[64 + threadIdx.x], c = red[128 + threadIdx.x], d = red[192 + threadIdx.x];
-    const float sx = ((a.x + b.x) + c.x) + d.x, sy = ((a.y + b.y) + c.y) + d.y;
     const float tau = prm[(size_t)i * br.prm_f];
     const float nx = sqrtf(sx), ny = sqrtf(sy);
     fmap[(size_t)i * kE + e] = make_float2(bt_f(tau, __builtin_amdgcn_rcpf(nx)), bt_f(tau, __builtin_amdgcn_rcpf(ny)));

@@ -106,9 +106,10 @@ hipError_t launch_plane_iso(const float* y, float* x_out, const void* tables, bo
 }
 
 hipError_t launch_iso_norm(const float2* qpart, float2* fmap, float2* nrm, const float* prm, size_t planes,
-                           hipStream_t s, const Branches* brp) {
+                           hipStream_t s, const Branches* brp, float2* sum_out, const float2* sum_in) {
     const Branches br = brp ? *brp : Branches{(int)planes, 1, 1, 0u, 0u};
-    hipLaunchKernelGGL(iso_norm_kernel, dim3(64 * kPT / 64, (unsigned)br.nbr), dim3(256), 0, s, qpart, fmap, nrm, prm, br);
+    hipLaunchKernelGGL(iso_norm_kernel, dim3(64 * kPT / 64, (unsigned)br.nbr), dim3(256), 0, s, qpart, fmap, nrm, prm, br,
+                       sum_out, sum_in);
     return hipGetLastError();
 }
 

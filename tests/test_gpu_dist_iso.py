@@ -1,7 +1,9 @@
 """GPU: the isotropic prox over a batch sharded across 2 processes sharing the one GPU (gloo carries
 the M x N maps through admm_batch_reducer; on a multi-GPU node the same call runs over RCCL).
 The shards must reassemble the single-process solve of the whole batch (forward and adjoint), up to
-the fp32 rounding of the differently ordered batch sums."""
+the fp32 rounding of the differently ordered batch sums.  64^2 runs the 2-pass kernels; 256^2 the
+split-iteration kernels of plane_iso.hip (their batch sums split into shard sum / all-reduce / factor),
+with the fused reverse sweep when rho_bar is not requested."""
 import os
 import socket
 
@@ -16,22 +18,22 @@ from admm_deconv import parallel, synth
 
 pytestmark = pytest.mark.gpu
 
-B, M, N, K = 6, 64, 64, 8
+B, K = 6, 8
 LAM, RHO = 0.0041, 0.021
 
 
-def _inputs():
+def _inputs(M):
     h = synth.gaussian_psf(7, 1.2)
-    y = synth.make_batch(B, M, N, h)
+    y = synth.make_batch(B, M, M, h)
     xbar = np.random.default_rng(11).standard_normal(y.shape).astype(np.float32)
     return h, y, xbar
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, M, need_rho):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    h, y, xbar = _inputs()
+    h, y, xbar = _inputs(M)
     start, count = parallel.shard_range(B, world, rank)
     dev = torch.device("cuda", 0)
     ys = torch.from_numpy(y[start:start + count]).to(dev)
@@ -39,9 +41,11 @@ def _worker(rank, world, port, q):
     ht = torch.from_numpy(h).to(dev)
     g = dist.group.WORLD
     x = admm_deconv.tvd_fft(ys, LAM, RHO, ht, True, K, group=g)
-    x2, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(ys, xb, LAM, RHO, ht, True, K, group=g)
+    x2, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(ys, xb, LAM, RHO, ht, True, K, group=g, need_h=need_rho,
+                                                      need_rho=need_rho)
     torch.cuda.synchronize()
-    q.put((rank, x.cpu().numpy(), x2.cpu().numpy(), yb.cpu().numpy(), hb.cpu().numpy(), float(lb), float(rb)))
+    q.put((rank, x.cpu().numpy(), x2.cpu().numpy(), yb.cpu().numpy(), None if hb is None else hb.cpu().numpy(),
+           float(lb), None if rb is None else float(rb)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,17 +62,20 @@ def _rel(a, b):
     return float(np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b))
 
 
-def test_iso_sharded_two_processes(dev):
-    h, y, xbar = _inputs()
+@pytest.mark.parametrize("M,need_rho", [(64, True), (256, True), (256, False)],
+                         ids=["2pass", "fused-fwd", "fused-fwd+sweep"])
+def test_iso_sharded_two_processes(dev, M, need_rho):
+    h, y, xbar = _inputs(M)
     ht = torch.from_numpy(h).to(dev)
     x0 = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), LAM, RHO, ht, True, K).cpu().numpy()
     _, yb0, hb0, lb0, rb0 = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev),
-                                                        torch.from_numpy(xbar).to(dev), LAM, RHO, ht, True, K)
-    yb0, hb0, lb0, rb0 = yb0.cpu().numpy(), hb0.cpu().numpy(), float(lb0), float(rb0)
+                                                        torch.from_numpy(xbar).to(dev), LAM, RHO, ht, True, K,
+                                                        need_h=need_rho, need_rho=need_rho)
+    yb0, lb0 = yb0.cpu().numpy(), float(lb0)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, M, need_rho)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
@@ -79,6 +86,9 @@ def test_iso_sharded_two_processes(dev):
     assert _rel(x, x0) < 1e-5
     assert _rel(np.concatenate([r[2] for r in res]), x0) < 1e-5
     assert _rel(np.concatenate([r[3] for r in res]), yb0) < 1e-4
-    assert _rel(sum(r[4] for r in res), hb0) < 1e-3
     assert abs(sum(r[5] for r in res) - lb0) <= 1e-3 * abs(lb0)
-    assert abs(sum(r[6] for r in res) - rb0) <= 1e-3 * abs(rb0)
+    if need_rho:
+        assert _rel(sum(r[4] for r in res), hb0.cpu().numpy()) < 1e-3
+        assert abs(sum(r[6] for r in res) - float(rb0)) <= 1e-3 * abs(float(rb0))
+    else:
+        assert rb0 is None and all(r[6] is None for r in res)
