@@ -185,3 +185,13 @@ def test_multi_branch_workspace_and_validation():
     f = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, 0)
     m = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, _lib.REC_MASKS)
     assert m < f
+    # isotropic (ADMM_MULTI_ISO): f maps and q partials on top of the plain layout; a recording keeps s_k
+    # itself (the BT derivative needs it), |s_k| per branch and the R maps -- ADMM_REC_MASKS does not shrink it
+    iso = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_ISO)
+    assert iso - plain >= 5 * px * 4 + planes * px * 4
+    iso_rec = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_ISO | _lib.MULTI_RECORD)
+    assert iso_rec - full >= 49 * 5 * px * 4
+    assert _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_ISO | _lib.MULTI_RECORD | _lib.REC_MASKS) == iso_rec
+    # the single-solve isotropic recording without rho_bar (the fused sweep) keeps the full-size trajectory
+    fi = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, True, 50, 0)
+    assert _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, True, 50, _lib.REC_MASKS) == fi
