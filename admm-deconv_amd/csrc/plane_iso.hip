@@ -13,6 +13,9 @@
 //       A phase  s_{k+1} = D x_{k+1} + (s_k - f_k s_k) stored, q = sum over channels of s_{k+1}^2  (row_iso_a)
 //       (k = 0 starts from y: H^T y, line forward; the last launch writes x instead of the A phase)
 //   iso_norm_kernel(k+1)     |s_{k+1}| = sqrt(sum over the branch's planes of q), f_{k+1} = max(1 - tau/|s|, 0)
+//                            (bt_f; a sharded batch splits it: shard sums, the caller's all-reduce, factor)
+// Recording for the reverse sweep (below): s_{k+1} goes to trajectory slot k instead of in place, and
+// |s_{k+1}| to norm slot k.
 // Every per-pixel map is lane-native like s (element (register n, thread t) at [n][t], float2 = the
 // lane's pixel pair), so all of it is read and written in whole-wave contiguous runs.
 // HBM per pixel and iteration: B phase s_k 8 + H^T y 4, A phase s_k 8 + s_{k+1} 8 + q 4, norm q 4 (f, the
