@@ -141,6 +141,11 @@ int devtest_plane_timing(const float* y, float* x, const float* Cf, const float*
                          float tau, float rho, int K, int planes, float* dbg) {
     return plane_debug<2>(y, x, Cf, C0b, hln, sln, tau, rho, K, planes, dbg);
 }
+// workgroup start / end only (slots 508 / 509 of wave 0, s_memrealtime), the product kernel otherwise
+int devtest_plane_wg_times(const float* y, float* x, const float* Cf, const float* C0b, float* hln, float* sln,
+                           float tau, float rho, int K, int planes, float* dbg) {
+    return plane_debug<3>(y, x, Cf, C0b, hln, sln, tau, rho, K, planes, dbg);
+}
 #ifdef PLANE_TS
 int devtest_plane_ts_set(unsigned long long* buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(admm::plane::g_plane_ts), &buf, sizeof(buf)) == hipSuccess ? 0 : -4;

@@ -561,7 +561,8 @@ __device__ __forceinline__ void column_phase(float2 (&S)[64], float2* colbuf, co
 }
 
 // debug aid (devtest only): DBG == 1 dumps S after each phase of every iteration (plane 0);
-// DBG == 2 records the shader clock at each phase boundary (lane 0 of every wave, every plane).
+// DBG == 2 records the shader clock at each phase boundary (lane 0 of every wave, every plane);
+// DBG == 3 only the workgroup start / end (slots 508 / 509), otherwise the product kernel.
 template <int DBG>
 __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int slot, int t) {
     if constexpr (DBG == 2) {
@@ -611,6 +612,10 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
     // late, so that the memory-heavy row phases of two groups of CUs interleave.
+    if constexpr (DBG >= 2) {   // workgroup start / end on the constant 100 MHz clock (slots 508 / 509 of wave 0)
+        if (threadIdx.x == 0)
+            reinterpret_cast<unsigned long long*>(dbg)[(size_t)blockIdx.x * 8 * 512 + 508] = __builtin_amdgcn_s_memrealtime();
+    }
     if (stagger_ticks > 0 && (blockIdx.x & 1)) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger_ticks) __builtin_amdgcn_s_sleep(10);
@@ -667,7 +672,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
         // the last iteration keeps x in registers for the output; the others hand x[32..63] to the
         // row phase's LDS staging slots directly (no spill of the line inverse's peak)
-        constexpr bool kStage = DBG == 0 && PLANE_STAGE_INV;
+        constexpr bool kStage = (DBG == 0 || DBG == 3) && PLANE_STAGE_INV;
         if constexpr (!kStage) {
             line_inverse_pair(S, hb);
             dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
@@ -718,6 +723,10 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     float2* xrow = reinterpret_cast<float2*>(x_out + bo.out_plane * 65536 + (size_t)r * 256);
 #pragma unroll
     for (int n = 0; n < 64; ++n) xrow[2 * n + hb] = S[n];
+    if constexpr (DBG >= 2) {
+        if (threadIdx.x == 0)
+            reinterpret_cast<unsigned long long*>(dbg)[(size_t)blockIdx.x * 8 * 512 + 509] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 
