@@ -19,10 +19,10 @@ ADMM_E_HIP = -4
 ADMM_E_REDUCER = -5
 
 # library options (admm_set_option, include/admm_deconv.h)
-OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER, OPT_SMOOTH = range(8)
+OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER, OPT_SMOOTH, OPT_RESIDENT = range(9)
 OPTIONS = {"FUSED": OPT_FUSED, "FUSED_ADJ": OPT_FUSED_ADJ, "LINE_T": OPT_LINE_T, "COL_THREADS": OPT_COL_THREADS,
            "GEN_TM": OPT_GEN_TM, "GEN_KN": OPT_GEN_KN, "PLANE_STAGGER": OPT_PLANE_STAGGER,
-           "SMOOTH": OPT_SMOOTH}
+           "SMOOTH": OPT_SMOOTH, "RESIDENT": OPT_RESIDENT}
 
 K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE, K_ADJ = range(8)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",

@@ -28,6 +28,7 @@
 #include "admm_generic_bwd.hip"
 #include "plane_api.hpp"
 #include "smooth_api.hpp"
+#include "resident_api.hpp"
 #include "layout.hpp"
 
 namespace {
@@ -62,7 +63,7 @@ constexpr int kGenMax = 4096;
 // Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
 // choices; the others exist for tests (fused vs 2-pass) and tuning experiments.  A recording stores
 // the option values it was made with, and its replay rejects a change (RecTag below).
-std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}};
+std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}};
 int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 
 // ADMM_OPT_FUSED = 0 forces the 2-pass path (tests compare the two).
@@ -636,9 +637,15 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             return 0;
         });
     };
+    // CU-resident solve (admm_resident.hip): anisotropic, no dim-2 spectra or isotropic norms recorded; it
+    // forms the first line spectrum itself, so PREP only produces H^T y
+    const bool res = !iso && !tr.v && !tr.nrm && !tr.m && opt(ADMM_OPT_RESIDENT) != 0 && opt(ADMM_OPT_SMOOTH) != 0 &&
+                     admm::rs::has_shape(M, N);
     // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
-    rc = line_fwd(y, spec0);
-    if (rc) return rc;
+    if (!res || kh > 0) {
+        rc = line_fwd(y, spec0);
+        if (rc) return rc;
+    }
     if (kh > 0) {
         rc = ln.run(ADMM_K_PREP, [&] {
             if (smc) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 1, opt(ADMM_OPT_SMOOTH));
@@ -652,11 +659,18 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             return 0;
         });
         if (rc) return rc;
-        rc = line_fwd(hty, spec0);
-        if (rc) return rc;
+        if (!res) {
+            rc = line_fwd(hty, spec0);
+            if (rc) return rc;
+        }
     }
     const int ng = iso_ngroups(planes);
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
+    if (res) {
+        return ln.run(ADMM_K_PLANE, [&] {
+            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit);
+        });
+    }
     for (int it = 1; it <= maxit; ++it) {
         // trajectory for h_bar: the dim-2 spectrum of iteration it before the multiply
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * planes * N * H : nullptr;

@@ -1,0 +1,671 @@
+// admm_resident.hip -- the whole K-iteration anisotropic ADMM solve of ONE plane per workgroup for smooth
+// non-power-of-two sides <= 256 (reference: tvd_fft_cpu / tvd_fft_gpu, /root/reference/src/ops/ops.jl:46-93 /
+// :132-176; any M x N through FFTW / CUFFT plans, ops.jl:26,86).
+//
+// Why: the smooth 2-pass path (admm_smooth.hip) moves the line spectrum through HBM twice per iteration
+// (44 B/px/iter at 250^2: column pass 8, line inverse 8, update 28).  Here the half spectrum never leaves the
+// CU: 512 threads hold it in registers (250^2: 126 bins x 250 lines = 63 float2 per thread) and the
+// transforms run in LDS, one chunk at a time.  Per iteration the only HBM traffic is the ADMM state
+// s = Dx + u (read + write, 8 B/px each) and H^T y (4 B/px): 20 B/px, as in the 256^2 kernel
+// (plane_kernel.hip).
+//
+// Register layout: thread t = k * LS + jt (LS = 512 / H line slots) holds bin k of lines jt, jt + LS, ...:
+// S[r] = X(line r LS + jt, bin k).  So a bin's column lives in LS threads at consecutive registers and a
+// line chunk is a fixed register range: both staging directions are plain LDS stores at compile-time
+// offsets, no index arithmetic per element.
+//
+// Per iteration:
+//   column phase  per chunk of KBC bins: S -> LDS [bin][line], dim-2 FFT (compile-time Stockham plan,
+//                 fft_smooth.hpp), x Ct (C / (MN), ops.jl:86) fused between the last forward and the first
+//                 inverse pass, IFFT, LDS -> S.
+//   line phase    per chunk of T lines plus the two halo lines either side (T + 2 rows): S -> LDS, paired
+//                 real inverse transforms -> x rows; then every wave walks its own rows:
+//                 s = D x + clip(s_old) (ops.jl:87-92 with u = clip(s)), w = z - u, v = H^T y + rho D^T w,
+//                 s stored, v written over x (a wave's first and last rows only after a block barrier: they
+//                 are the rows its neighbours read); paired forward transforms of v -> S.
+// H^T y itself (with a PSF: F^-1 conj(Sigma_c) F y, ops.jl:71-81) comes from the 2-pass PREP kernels; the
+// first iteration's spectrum is its line rFFT, formed here.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "fft_smooth.hpp"
+#include "resident_api.hpp"
+
+namespace admm {
+namespace rs {
+
+using sm::dftR;
+using sm::SP;
+
+constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
+constexpr int kRad = 16;                  // radix cap of every transform
+constexpr int kLdsBytes = 160 * 1024;     // gfx950 LDS per CU
+
+constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
+constexpr int imax(int a, int b) { return a > b ? a : b; }
+constexpr int imin(int a, int b) { return a < b ? a : b; }
+
+__device__ __forceinline__ float clipf(float s, float tau) { return fminf(fmaxf(s, -tau), tau); }
+// w = z - u for z = ST(s, tau), u = s - z  (ops.jl:9, :171-173)
+__device__ __forceinline__ float prox_w(float s, float tau) { return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s; }
+
+// Buffer resources for the update's HBM traffic (32-bit offsets: a wave-uniform row offset in an SGPR and
+// a per-lane constant pixel offset; out-of-range loads return 0)
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld1(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+__device__ __forceinline__ void bst1(rsrc_t r, unsigned vo, unsigned so, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+}
+
+// The thread index through an opaque move: values derived from it are recomputed inside the iteration loop
+// rather than hoisted out of it (dozens of per-pass start indices and LDS bases would otherwise stay live
+// across all K iterations, next to the 126-VGPR spectrum)
+__device__ __forceinline__ int tid() {
+    int y;
+    __asm__ volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"((int)threadIdx.x));
+    return y;
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// ---- in-place mixed-radix transforms -------------------------------------------------------------------
+// Radices R_0 .. R_{P-1} (fft_smooth.hpp's plan, increasing, <= kRad).  Pass p works on blocks of
+// L_p = LEN / (R_0 .. R_{p-1}) points with stride S_p = L_p / R_p.
+//   DIF pass (natural order in): load x[base + r S], DFT over r, x W_L^{j m}, store at base + m S;
+//   DIT pass: load at base + m S, x W_L^{j m}, DFT over m, store at base + r S  (base = block L + j).
+// DIF passes 0 .. P-1 leave frequency k = m_0 + R_0 m_1 + R_0 R_1 m_2 + .. at position
+// pos(k) = m_0 S_0 + m_1 S_1 + ..; DIT passes P-1 .. 0 undo them (conjugate kernels: an unnormalised
+// inverse).  Every butterfly reads and writes the same R slots, so a pass needs no barrier of its own and
+// holds only R complex values per butterfly -- the spectrum's registers stay free.
+template <int LEN>
+struct Rad {
+    using S = SP<LEN, true, kRad>;
+    static constexpr int P = S::P;
+    static constexpr int r(int p) { return S::pl.r[p]; }
+    static constexpr int L(int p) {
+        int l = LEN;
+        for (int q = 0; q < p; ++q) l /= r(q);
+        return l;
+    }
+    static constexpr int st(int p) { return L(p) / r(p); }   // S_p
+    static constexpr int W(int p) {                           // R_0 .. R_{p-1}
+        int w = 1;
+        for (int q = 0; q < p; ++q) w *= r(q);
+        return w;
+    }
+};
+
+// position of natural index k after the DIF passes
+template <int LEN>
+__device__ __forceinline__ int dpos(int k) {
+    using RD = Rad<LEN>;
+    int pos = 0;
+    static_for<0, RD::P>([&](auto ip) {
+        constexpr int p = decltype(ip)::value;
+        constexpr int R = RD::r(p);
+        const int q = k / R;
+        pos += (k - q * R) * RD::st(p);
+        k = q;
+    });
+    return pos;
+}
+// frequency of slot b R + m after the DIF passes (b = butterfly of the last pass): kbase(b) + m W_{P-1}
+template <int LEN>
+__device__ __forceinline__ int dlast(int b) {
+    using RD = Rad<LEN>;
+    int k = 0;
+    static_for<0, RD::P - 1>([&](auto ip) {
+        constexpr int p = RD::P - 2 - decltype(ip)::value;   // least significant digit of b first
+        constexpr int R = RD::r(p);
+        const int q = b / R;
+        k += (b - q * R) * RD::W(p);
+        b = q;
+    });
+    return k;
+}
+
+template <bool INV>
+__device__ __forceinline__ float2 twv(const float2* __restrict__ tw, int e) {
+    float2 w = tw[e];
+    if (INV) w.y = -w.y;
+    return w;
+}
+
+// Accessor of cnt transforms: transform f point n at base[f * FS + n]
+template <int FS>
+struct Acc {
+    float2* base;
+    __device__ __forceinline__ float2 ld(int f, int n) const { return base[f * FS + n]; }
+    __device__ __forceinline__ void st(int f, int n, float2 v) const { base[f * FS + n] = v; }
+};
+
+// one in-place pass p over cnt transforms; butterflies dealt to the block's threads two at a time.
+// FMAJ: consecutive threads take one transform's consecutive butterflies (lines); else consecutive
+// transforms (columns).
+template <int LEN, int p, bool DIT, bool INV, bool FMAJ, int FS>
+__device__ __forceinline__ void ipass(int cnt, const float2* __restrict__ tw, Acc<FS> a) {
+    using RD = Rad<LEN>;
+    constexpr int R = RD::r(p), L = RD::L(p), S = L / R, Q = LEN / R, TS = LEN / L;
+    const int total = cnt * Q;
+    auto where = [&](int idx, int& f, int& base, int& j) {
+        int b;
+        if (FMAJ) {
+            f = idx / Q;
+            b = idx - f * Q;
+        } else {
+            b = idx / cnt;
+            f = idx - b * cnt;
+        }
+        const int blk = b / S;
+        j = b - blk * S;
+        base = blk * L + j;
+    };
+    auto fly = [&](float2 (&v)[R], int j) {
+        if constexpr (DIT && S > 1) {
+#pragma unroll
+            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tw, j * m * TS));
+        }
+        dftR<R, INV>(v);
+        if constexpr (!DIT && S > 1) {
+#pragma unroll
+            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tw, j * m * TS));
+        }
+    };
+    for (int i0 = tid(); i0 < total; i0 += 2 * kNT) {
+        const int i1 = i0 + kNT;
+        int f0, b0, j0, f1 = 0, b1 = 0, j1 = 0;
+        where(i0, f0, b0, j0);
+        const bool two = i1 < total;
+        if (two) where(i1, f1, b1, j1);
+        float2 v0[R], v1[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v0[r] = a.ld(f0, b0 + r * S);
+        if (two) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v1[r] = a.ld(f1, b1 + r * S);
+        }
+        fly(v0, j0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) a.st(f0, b0 + r * S, v0[r]);
+        if (two) {
+            fly(v1, j1);
+#pragma unroll
+            for (int r = 0; r < R; ++r) a.st(f1, b1 + r * S, v1[r]);
+        }
+    }
+}
+
+// DIF passes [p0, p1) / DIT passes (p1 .. p0], a block barrier after each
+template <int LEN, int p0, int p1, bool INV, bool FMAJ, int FS>
+__device__ __forceinline__ void dif_passes(int cnt, const float2* tw, Acc<FS> a) {
+    static_for<p0, p1>([&](auto ip) {
+        ipass<LEN, decltype(ip)::value, false, INV, FMAJ, FS>(cnt, tw, a);
+        __syncthreads();
+    });
+}
+template <int LEN, int p0, int p1, bool INV, bool FMAJ, int FS>
+__device__ __forceinline__ void dit_passes(int cnt, const float2* tw, Acc<FS> a) {
+    static_for<p0, p1>([&](auto ip) {
+        ipass<LEN, p1 - 1 - (decltype(ip)::value - p0), true, INV, FMAJ, FS>(cnt, tw, a);
+        __syncthreads();
+    });
+}
+
+template <int MM, int NN>
+struct Geo {
+    static constexpr int H = MM / 2 + 1;           // bins per line
+    static constexpr int LS = (kNT / H) & ~1;      // line slots (even: lines 2f, 2f + 1 in neighbouring lanes)
+    static constexpr int NR = cdiv(NN, LS);        // spectrum registers per thread
+    static constexpr int FS = NN | 1;              // column stride (odd: neighbouring columns on distinct banks)
+    static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
+    static constexpr int kBudget = (kLdsBytes - 512) / 8 - MM - NN;   // float2 slots for the main buffer
+    static constexpr int ncc() {
+        for (int n = 1; n <= H; ++n)
+            if (cdiv(H, n) * FS <= kBudget) return n;
+        return 0;
+    }
+    static constexpr int tl(int n) { return (cdiv(NN, n) + 1) & ~1; }
+    static constexpr int nlc() {   // line chunks: T lines + a halo pair either side, as complex line pairs
+        for (int n = 1; n <= NN; ++n)
+            if ((tl(n) / 2 + 2) * MM <= kBudget) return n;
+        return 0;
+    }
+    static constexpr int NCC = ncc();              // column chunks
+    static constexpr int KBC = cdiv(H, NCC);       // bins per column chunk
+    static constexpr int NLC = nlc();              // line chunks
+    static constexpr int TL = tl(NLC);             // lines per line chunk (even)
+    static constexpr int BUF = imax(KBC * FS, (TL / 2 + 2) * MM);
+    static constexpr size_t lds_bytes() { return (size_t)(MM + NN + BUF) * 8; }
+    static_assert(MM % 2 == 0 && NN % 2 == 0 && MM <= 256 && NN <= 256, "resident kernel: even M, N <= 256");
+    static_assert(LS >= 2 && NCC >= 1 && NLC >= 1, "resident kernel: shape does not fit one CU");
+    static_assert(Rad<MM>::P >= 2 && Rad<NN>::P >= 2, "plans of >= 2 passes");
+};
+
+struct Thr {
+    float2* buf;          // main LDS buffer
+    const float2* twm;    // LDS twiddles exp(-2 pi i n / M), exp(-2 pi i n / N)
+    const float2* twn;
+    int k, jt;            // bin, line slot
+    bool act;             // t < H LS
+};
+template <int MM, int NN>
+__device__ __forceinline__ Thr thr_of(float2* buf, const float2* twm, const float2* twn) {
+    constexpr int H = MM / 2 + 1, LS = (kNT / H) & ~1;
+    const unsigned t = (unsigned)tid();
+    return {buf, twm, twn, (int)(t / LS), (int)(t % LS), t < (unsigned)(H * LS)};
+}
+
+// ---- column phase, chunk C: bins [kc0, kc1) --------------------------------------------------------------
+template <int MM, int NN, int C, int NR>
+__device__ __forceinline__ void column_chunk(float2 (&S)[NR], const Thr& th0, const float* __restrict__ Ct) {
+    using G = Geo<MM, NN>;
+    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
+    using RD = Rad<NN>;
+    constexpr int kc0 = C * G::KBC, kc1 = imin(G::H, kc0 + G::KBC), kc = kc1 - kc0;
+    constexpr int KB = G::KBC, FS = G::FS, H = G::H, P = RD::P;
+    float2* buf = th.buf;
+    const bool mine = th.act && th.k >= kc0 && th.k < kc1;
+    if (mine) {
+        float2* col = buf + (th.k - kc0) * FS;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int j = r * G::LS + th.jt;
+            if (r < NR - 1 || j < NN) col[j] = S[r];
+        }
+    }
+    __syncthreads();
+    const Acc<FS> a{buf};
+    dif_passes<NN, 0, P - 1, false, false, FS>(KB, th.twn, a);
+    // last DIF pass (S = 1: no twiddles) -> x Ct at the slot's frequency -> first DIT pass, in registers
+    {
+        constexpr int R = RD::r(P - 1), Q = NN / R, WL = RD::W(P - 1);
+        for (int idx = tid(); idx < KB * Q; idx += kNT) {
+            const int b = idx / KB, f = idx - b * KB;
+            const float* cp = Ct + (size_t)dlast<NN>(b) * H + kc0 + (f < kc ? f : 0);
+            float cm[R];
+#pragma unroll
+            for (int m = 0; m < R; ++m) cm[m] = cp[(size_t)m * WL * H];
+            float2 v[R];
+#pragma unroll
+            for (int m = 0; m < R; ++m) v[m] = a.ld(f, b * R + m);
+            dftR<R, false>(v);
+#pragma unroll
+            for (int m = 0; m < R; ++m) v[m] = cscale(v[m], cm[m]);
+            dftR<R, true>(v);
+#pragma unroll
+            for (int m = 0; m < R; ++m) a.st(f, b * R + m, v[m]);
+        }
+    }
+    __syncthreads();
+    dit_passes<NN, 0, P - 1, true, false, FS>(KB, th.twn, a);
+    if (mine) {
+        const float2* col = buf + (th.k - kc0) * FS;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int j = r * G::LS + th.jt;
+            if (r < NR - 1 || j < NN) S[r] = col[j];
+        }
+    }
+    __syncthreads();
+}
+
+// ---- line phase, chunk C: lines [jc0, jc1) ---------------------------------------------------------------
+// Lines are held as complex pairs z_f = line 2f + i line 2f+1 (both spectra with their Hermitian
+// extensions folded in, then both real lines after the inverse), M float2 per pair.  Update mode stages
+// the chunk plus the halo pairs (jc0 - 2, jc0 - 1) and (jc1, jc1 + 1): pair u / 2 of staged line u.
+enum Mode { kInit = 0, kUpdate = 1, kFinal = 2 };
+
+struct LineArgs {
+    const float* hty;     // this plane's H^T y
+    const float* so;      // s_old (channel 0; channel 1 at + MN), unused when first
+    float* sn;            // s_new
+    float* xo;            // x out (final)
+    float tau, rho;
+    bool first;
+};
+
+__device__ __forceinline__ float2 lane_swap(float2 v) {   // value of lane t ^ 1 (DPP quad_perm [1, 0, 3, 2])
+    const int x = __builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0xB1, 0xF, 0xF, true);
+    const int y = __builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, true);
+    return make_float2(__int_as_float(x), __int_as_float(y));
+}
+
+// Per-thread constants of the pair staging / separation (branch-free, so a register's store is one
+// ds_write at a compile-time offset from the thread's base)
+struct ZLane {
+    int slot;        // z slot this lane writes: k (even line) or M - k (odd line)
+    bool wr;         // odd lanes skip DC and Nyquist (their z slot is the even lane's)
+    float sgn;       // +1 even, -1 odd
+    float im;        // 0 at DC / Nyquist (a real line's inverse keeps only the real parts), else 1
+    bool odd;
+};
+template <int MM>
+__device__ __forceinline__ ZLane zlane(int k, bool odd) {
+    const bool edge = k == 0 || 2 * k == MM;
+    return {odd ? (edge ? k : MM - k) : k, !odd || !edge, odd ? -1.0f : 1.0f, edge ? 0.0f : 1.0f, odd};
+}
+// own X_j(k) and the partner lane's X_{j^1}(k) -> z value: even line z[k] = X_2f + i X_2f+1,
+// odd line z[M - k] = conj X_2f + i conj X_2f+1 (Hermitian extension)
+__device__ __forceinline__ float2 zval(float2 x, float2 o, const ZLane& zl) {
+    const float2 a = zl.odd ? o : x;   // X_2f
+    const float2 b = zl.odd ? x : o;   // X_2f+1
+    return make_float2(fmaf(-zl.sgn * zl.im, b.y, a.x), fmaf(zl.sgn * zl.im, a.y, b.x));
+}
+// separation from z (bin k) and z' = z(M - k): even line X = (z + conj z') / 2, odd X = (z - conj z') / (2i)
+__device__ __forceinline__ float2 zsep(float2 z, float2 zm, bool odd) {
+    const float px = odd ? z.y : z.x, py = odd ? -z.x : z.y;
+    const float qx = odd ? zm.y : zm.x, qy = odd ? zm.x : -zm.y;
+    return make_float2(0.5f * (px + qx), 0.5f * (py + qy));
+}
+
+// hs[c]: chunk c's halo-A register (lines jc0 - 2, jc0 - 1) for c >= 1, hs[0] the register of lines 0, 1 (the
+// last chunk's halo B), saved before the update phase: by the time a chunk stages them, the chunk that owns
+// those lines has already replaced them with the next iteration's spectra.
+template <int MM, int NN, int C, int MODE, int NR, int NH>
+__device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[NH], const Thr& th0, const LineArgs& a) {
+    using G = Geo<MM, NN>;
+    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
+    using RD = Rad<MM>;
+    constexpr int LS = G::LS, P = RD::P;
+    constexpr int jc0 = C * G::TL, jc1 = imin(NN, jc0 + G::TL), T = jc1 - jc0;
+    constexpr int HP = MODE == kUpdate ? 1 : 0;   // halo pairs either side
+    constexpr int NP = T / 2 + 2 * HP;            // pairs staged
+    float2* buf = th.buf;
+    float* Xf = reinterpret_cast<float*>(buf);
+    const Acc<MM> al{buf};
+
+    if constexpr (MODE != kInit) {
+        // ---- S -> z pairs, inverse DIF (x at dpos order) ----
+        if (th.act) {
+            const ZLane zl = zlane<MM>(th.k, th.jt & 1);
+            float2* zb = buf + (th.jt >> 1) * MM + zl.slot;   // + pair offset of register r
+#pragma unroll
+            for (int r = jc0 / LS; r <= (jc1 - 1) / LS; ++r) {
+                const int j = r * LS + th.jt;
+                const float2 z = zval(S[r], lane_swap(S[r]), zl);
+                if (zl.wr && (r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1))
+                    zb[((r * LS - jc0) / 2 + HP) * MM] = z;
+            }
+            if constexpr (HP) {
+                constexpr int hA = (jc0 + NN - 2) % NN, hB = jc1 % NN;   // even lines: pairs (hA, hA+1), (hB, hB+1)
+                const float2 sA = C >= 1 ? hs[C] : S[hA / LS];
+                const float2 zA = zval(sA, lane_swap(sA), zl);
+                if (zl.wr && (th.jt >> 1) == (hA % LS) / 2) buf[zl.slot] = zA;
+                const float2 sB = (C == G::NLC - 1 && G::NLC > 1) ? hs[0] : S[hB / LS];
+                const float2 zB = zval(sB, lane_swap(sB), zl);
+                if (zl.wr && (th.jt >> 1) == (hB % LS) / 2) buf[(NP - 1) * MM + zl.slot] = zB;
+            }
+        }
+        __syncthreads();
+        dif_passes<MM, 0, P, true, true, MM>(NP, th.twm, al);
+    }
+
+    if constexpr (MODE == kFinal) {
+        // x rows out in natural pixel order (pair (j - jc0) / 2, real part for even j)
+        float* xo = a.xo + (size_t)jc0 * MM;
+        for (int idx = tid(); idx < T * MM; idx += kNT) {
+            const int u = idx / MM, i = idx - u * MM;
+            xo[idx] = Xf[2 * ((u >> 1) * MM + dpos<MM>(i)) + (u & 1)];
+        }
+        __syncthreads();
+        return;
+    }
+
+    if constexpr (MODE == kUpdate) {
+        // ---- row update: wave w walks staged lines ua .. ub (staged line u = line jc0 + u - 2) ----
+        // Global traffic through buffer resources: the row offset is wave-uniform (soffset), the lane's
+        // pixel offset a per-lane constant (voffset), so no 64-bit address per load.
+        constexpr int QN = G::QN;
+        constexpr unsigned MN = (unsigned)MM * NN;
+        const int t = tid();
+        const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+        const int lane = t & 63;
+        const int ua = 2 + (w * T) / 8, ub = 1 + ((w + 1) * T) / 8;
+        const float tau = a.tau, rho = a.rho;
+        const rsrc_t rso = make_rsrc(a.so, 2 * MN * 4), rsn = make_rsrc(a.sn, 2 * MN * 4), rh = make_rsrc(a.hty, MN * 4);
+        // float offsets of pixel i and its neighbours within a pair row (LDS), byte offset of i + 1 (HBM)
+        int pc[QN], pl[QN], pr[QN];
+        unsigned gr[QN];
+#pragma unroll
+        for (int q = 0; q < QN; ++q) {
+            const int i = lane + 64 * q < MM ? lane + 64 * q : 0;
+            pc[q] = 2 * dpos<MM>(i);
+            pl[q] = 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1);
+            pr[q] = 2 * dpos<MM>(i + 1 == MM ? 0 : i + 1);
+            gr[q] = 4u * (unsigned)(i + 1 == MM ? 0 : i + 1);
+        }
+        const unsigned gl = 4u * (unsigned)lane;   // + 256 q: the instruction's immediate offset
+        auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
+        auto valid = [&](int q) { return q < QN - 1 || lane + 64 * q < MM; };
+        float vf[QN], vl[QN];
+        if (ub >= ua) {
+            float w0c[QN];
+            {
+                const int j = jc0 + ua - 2;
+                const int ru = row(ua), rm = row(ua - 1);
+                const unsigned so = 4u * (unsigned)(j * MM);
+#pragma unroll
+                for (int q = 0; q < QN; ++q) {
+                    const float o = a.first ? 0.0f : bld1(rso, gl + 256 * q, so);
+                    const float s0 = (Xf[ru + pc[q]] - Xf[rm + pc[q]]) + clipf(o, tau);
+                    if (valid(q)) bst1(rsn, gl + 256 * q, so, s0);
+                    w0c[q] = prox_w(s0, tau);
+                }
+            }
+            struct GIn {
+                float a0n, a1, a1r, h;
+            };
+            auto gload = [&](GIn (&g)[QN], int u) {
+                const int j = jc0 + u - 2;
+                const int jn = j + 1 == NN ? 0 : j + 1;
+                const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
+#pragma unroll
+                for (int q = 0; q < QN; ++q) {
+                    g[q].h = bld1(rh, gl + 256 * q, oj);
+                    if (!a.first) {
+                        g[q].a0n = bld1(rso, gl + 256 * q, on);
+                        g[q].a1 = bld1(rso, gl + 256 * q, oj + 4 * MN);
+                        g[q].a1r = bld1(rso, gr[q], oj + 4 * MN);
+                    } else {
+                        g[q].a0n = g[q].a1 = g[q].a1r = 0.0f;
+                    }
+                }
+            };
+            GIn cur[QN], nxt[QN];
+            gload(cur, ua);
+#pragma unroll 1
+            for (int u = ua; u <= ub; ++u) {
+                if (u < ub) gload(nxt, u + 1);
+                const int j = jc0 + u - 2;
+                const int jn = j + 1 == NN ? 0 : j + 1;
+                const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
+                const int ru = row(u), rn = row(u + 1);
+                // every read of the row before any v is written over it: lanes read their neighbours'
+                // pixels, which other q slices of the same wave overwrite
+                float xcq[QN], xnq[QN], xlq[QN], xrq[QN];
+#pragma unroll
+                for (int q = 0; q < QN; ++q) {
+                    xcq[q] = Xf[ru + pc[q]];
+                    xnq[q] = Xf[rn + pc[q]];
+                    xlq[q] = Xf[ru + pl[q]];
+                    xrq[q] = Xf[ru + pr[q]];
+                }
+#pragma unroll
+                for (int q = 0; q < QN; ++q) {
+                    const float xc = xcq[q], xn = xnq[q], xl = xlq[q], xr = xrq[q];
+                    const float s0n = (xn - xc) + clipf(cur[q].a0n, tau);
+                    const float w0n = prox_w(s0n, tau);
+                    const float s1 = (xc - xl) + clipf(cur[q].a1, tau);
+                    if (valid(q)) {
+                        if (u < ub) bst1(rsn, gl + 256 * q, on, s0n);
+                        bst1(rsn, gl + 256 * q, oj + 4 * MN, s1);
+                    }
+                    const float w1 = prox_w(s1, tau);
+                    const float w1r = prox_w((xr - xc) + clipf(cur[q].a1r, tau), tau);
+                    const float v = fmaf(rho, (w0c[q] - w0n) + (w1 - w1r), cur[q].h);
+                    w0c[q] = w0n;
+                    if (u == ua) vf[q] = v;
+                    else if (u == ub) vl[q] = v;
+                    else if (valid(q)) Xf[ru + pc[q]] = v;
+                }
+#pragma unroll
+                for (int q = 0; q < QN; ++q) cur[q] = nxt[q];
+            }
+        }
+        __syncthreads();
+        if (ub >= ua) {
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+                if (valid(q)) {
+                    Xf[row(ua) + pc[q]] = vf[q];
+                    if (ub > ua) Xf[row(ub) + pc[q]] = vl[q];
+                }
+            }
+        }
+        __syncthreads();
+        // ---- forward DIT of the chunk's pairs (v at dpos order -> natural z) ----
+        dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, Acc<MM>{buf + MM});
+    } else {
+        // kInit: the first iteration's v = H^T y, from HBM into the pairs at dpos order
+        for (int idx = tid(); idx < T * MM / 2; idx += kNT) {
+            const int f = idx / MM, i = idx - f * MM;
+            const float* hp = a.hty + (size_t)(jc0 + 2 * f) * MM + i;
+            buf[f * MM + dpos<MM>(i)] = make_float2(hp[0], hp[MM]);
+        }
+        __syncthreads();
+        dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, al);
+    }
+    // ---- half spectra separated into S: X_2f = (z + conj z(-k)) / 2, X_2f+1 = (z - conj z(-k)) / (2i) ----
+    if (th.act) {
+        const int k = th.k, km = k == 0 ? 0 : MM - k;
+        const bool odd = th.jt & 1;
+        const float2* Zb = buf + ((th.jt >> 1) + HP) * MM;   // + pair offset of register r
+#pragma unroll
+        for (int r = jc0 / LS; r <= (jc1 - 1) / LS; ++r) {
+            const int j = r * LS + th.jt;
+            if ((r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1)) {
+                const float2* Z = Zb + ((r * LS - jc0) / 2) * MM;
+                S[r] = zsep(Z[k], Z[km], odd);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ---- the kernel: one workgroup per plane, all K iterations ---------------------------------------------------
+template <int MM, int NN>
+__global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__ hty_all, float* __restrict__ sA,
+                                                       float* __restrict__ sB, float* __restrict__ traj, size_t traj_stride,
+                                                       float* __restrict__ x_all, const float* __restrict__ Ct,
+                                                       const float2* __restrict__ twM, const float2* __restrict__ twN,
+                                                       const float* __restrict__ prm, int maxit) {
+    using G = Geo<MM, NN>;
+    constexpr int NR = G::NR;
+    constexpr size_t MN = (size_t)MM * NN;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* twm = reinterpret_cast<float2*>(smem_raw);
+    float2* twn = twm + MM;
+    for (int i = threadIdx.x; i < MM; i += kNT) twm[i] = twM[i];
+    for (int i = threadIdx.x; i < NN; i += kNT) twn[i] = twN[i];
+    const size_t plane = blockIdx.x;
+    const unsigned t = threadIdx.x;
+    Thr th;
+    th.buf = twn + NN;
+    th.twm = twm;
+    th.twn = twn;
+    th.k = (int)(t / G::LS);
+    th.jt = (int)(t % G::LS);
+    th.act = t < (unsigned)(G::H * G::LS);
+    LineArgs la;
+    la.hty = hty_all + plane * MN;
+    la.xo = x_all + plane * MN;
+    la.tau = prm[0];
+    la.rho = prm[1];
+    la.so = nullptr;
+    la.sn = nullptr;
+    la.first = true;
+    float2 S[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) S[r] = make_float2(0.f, 0.f);
+    __syncthreads();
+    float2 hs[G::NLC];
+    static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kInit>(S, hs, th, la); });
+#pragma unroll 1
+    for (int it = 1; it <= maxit; ++it) {
+#ifndef RS_SKIP_COL
+        static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+#endif
+        if (it == maxit) {
+            static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
+            break;
+        }
+        float* sn;
+        const float* so;
+        if (traj) {
+            sn = traj + (size_t)(it - 1) * traj_stride;
+            so = it >= 2 ? traj + (size_t)(it - 2) * traj_stride : sn;
+        } else {
+            sn = (it & 1) ? sA : sB;
+            so = (it & 1) ? sB : sA;
+        }
+        la.sn = sn + plane * 2 * MN;
+        la.so = so + plane * 2 * MN;
+        la.first = it == 1;
+        hs[0] = S[0];
+        static_for<1, G::NLC>([&](auto ic) {
+            constexpr int c = decltype(ic)::value;
+            hs[c] = S[(c * G::TL - 2) / G::LS];
+        });
+#ifndef RS_SKIP_UPD
+        static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kUpdate>(S, hs, th, la); });
+#endif
+    }
+}
+
+// ---- host side -----------------------------------------------------------------------------------------------
+// Shapes compiled here (M = line length, N = lines): square smooth sides the 2-pass path serves
+#ifndef RS_SHAPES_OVERRIDE
+#define RS_SHAPES(X) X(250, 250)
+#else
+#define RS_SHAPES(X) RS_SHAPES_OVERRIDE(X)
+#endif
+
+bool has_shape(int M, int N) {
+#define X(m, n) \
+    if (M == m && N == n) return true;
+    RS_SHAPES(X)
+#undef X
+    return false;
+}
+
+int launch(int M, int N, size_t planes, hipStream_t s, const float* hty, float* sA, float* sB, float* traj,
+           size_t traj_stride, float* x_out, const float* Ct, const float2* twM, const float2* twN, const float* prm,
+           int maxit) {
+#define X(m, n)                                                                                                  \
+    if (M == m && N == n) {                                                                                      \
+        constexpr size_t lds = Geo<m, n>::lds_bytes();                                                           \
+        (void)hipFuncSetAttribute((const void*)resident_kernel<m, n>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)lds);                                                                     \
+        resident_kernel<m, n><<<dim3((unsigned)planes), kNT, lds, s>>>(hty, sA, sB, traj, traj_stride, x_out, Ct, \
+                                                                        twM, twN, prm, maxit);                   \
+        return 0;                                                                                                \
+    }
+    RS_SHAPES(X)
+#undef X
+    return -1;
+}
+
+}  // namespace rs
+}  // namespace admm
