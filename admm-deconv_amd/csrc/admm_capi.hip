@@ -668,7 +668,8 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
     if (res) {
         return ln.run(ADMM_K_PLANE, [&] {
-            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit);
+            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit,
+                                    opt(ADMM_OPT_PLANE_STAGGER));
         });
     }
     for (int it = 1; it <= maxit; ++it) {

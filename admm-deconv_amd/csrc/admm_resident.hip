@@ -39,7 +39,13 @@ using sm::dftR;
 using sm::SP;
 
 constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
-constexpr int kRad = 16;                  // radix cap of every transform
+#ifndef RS_PD
+#define RS_PD 3                           // rows of update loads in flight ahead of the row being computed
+#endif
+#ifndef RS_RAD
+#define RS_RAD 16
+#endif
+constexpr int kRad = RS_RAD;              // radix cap of every transform
 constexpr int kLdsBytes = 160 * 1024;     // gfx950 LDS per CU
 
 constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -291,21 +297,35 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NR], const Thr& th0, co
     // last DIF pass (S = 1: no twiddles) -> x Ct at the slot's frequency -> first DIT pass, in registers
     {
         constexpr int R = RD::r(P - 1), Q = NN / R, WL = RD::W(P - 1);
-        for (int idx = tid(); idx < KB * Q; idx += kNT) {
-            const int b = idx / KB, f = idx - b * KB;
-            const float* cp = Ct + (size_t)dlast<NN>(b) * H + kc0 + (f < kc ? f : 0);
-            float cm[R];
+        constexpr int NB = cdiv(KB * Q, kNT);
+        // every multiplier load of the thread's butterflies first: one L2 latency per chunk, not one per butterfly
+        const int t0 = tid();
+        float cm[NB][R];
 #pragma unroll
-            for (int m = 0; m < R; ++m) cm[m] = cp[(size_t)m * WL * H];
-            float2 v[R];
+        for (int u = 0; u < NB; ++u) {
+            const int idx = t0 + u * kNT;
+            if (u < NB - 1 || idx < KB * Q) {
+                const int b = idx / KB, f = idx - b * KB;
+                const float* cp = Ct + (size_t)dlast<NN>(b) * H + kc0 + (f < kc ? f : 0);
 #pragma unroll
-            for (int m = 0; m < R; ++m) v[m] = a.ld(f, b * R + m);
-            dftR<R, false>(v);
+                for (int m = 0; m < R; ++m) cm[u][m] = cp[(size_t)m * WL * H];
+            }
+        }
 #pragma unroll
-            for (int m = 0; m < R; ++m) v[m] = cscale(v[m], cm[m]);
-            dftR<R, true>(v);
+        for (int u = 0; u < NB; ++u) {
+            const int idx = t0 + u * kNT;
+            if (u < NB - 1 || idx < KB * Q) {
+                const int b = idx / KB, f = idx - b * KB;
+                float2 v[R];
 #pragma unroll
-            for (int m = 0; m < R; ++m) a.st(f, b * R + m, v[m]);
+                for (int m = 0; m < R; ++m) v[m] = a.ld(f, b * R + m);
+                dftR<R, false>(v);
+#pragma unroll
+                for (int m = 0; m < R; ++m) v[m] = cscale(v[m], cm[u][m]);
+                dftR<R, true>(v);
+#pragma unroll
+                for (int m = 0; m < R; ++m) a.st(f, b * R + m, v[m]);
+            }
         }
     }
     __syncthreads();
@@ -450,7 +470,11 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
         auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
         auto valid = [&](int q) { return q < QN - 1 || lane + 64 * q < MM; };
         float vf[QN], vl[QN];
+#ifdef RS_SKIP_ROWS   // timing experiments only: no row update (wrong results)
+        if (false) {
+#else
         if (ub >= ua) {
+#endif
             float w0c[QN];
             {
                 const int j = jc0 + ua - 2;
@@ -483,11 +507,16 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                     }
                 }
             };
-            GIn cur[QN], nxt[QN];
-            gload(cur, ua);
+            // rows u + 1 .. u + RS_PD in flight while row u is computed (loads past the chunk read rows the
+            // next chunk or another wave owns, or beyond the plane, where the buffer returns 0: never used)
+            GIn pf[RS_PD][QN];
+#pragma unroll
+            for (int d = 0; d < RS_PD; ++d) gload(pf[d], ua + d);
 #pragma unroll 1
             for (int u = ua; u <= ub; ++u) {
-                if (u < ub) gload(nxt, u + 1);
+                GIn nx[QN];
+                gload(nx, u + RS_PD);
+                GIn (&cur)[QN] = pf[0];
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
                 const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
@@ -521,7 +550,11 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                     else if (valid(q)) Xf[ru + pc[q]] = v;
                 }
 #pragma unroll
-                for (int q = 0; q < QN; ++q) cur[q] = nxt[q];
+                for (int d = 0; d + 1 < RS_PD; ++d)
+#pragma unroll
+                    for (int q = 0; q < QN; ++q) pf[d][q] = pf[d + 1][q];
+#pragma unroll
+                for (int q = 0; q < QN; ++q) pf[RS_PD - 1][q] = nx[q];
             }
         }
         __syncthreads();
@@ -570,8 +603,15 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
                                                        float* __restrict__ sB, float* __restrict__ traj, size_t traj_stride,
                                                        float* __restrict__ x_all, const float* __restrict__ Ct,
                                                        const float2* __restrict__ twM, const float2* __restrict__ twN,
-                                                       const float* __restrict__ prm, int maxit) {
+                                                       const float* __restrict__ prm, int maxit, int stagger) {
     using G = Geo<MM, NN>;
+    // Phase groups (ADMM_OPT_PLANE_STAGGER): workgroup group g = (blockIdx / 8) % 4 starts g * stagger ticks of
+    // the 100 MHz realtime clock late, so that the groups' HBM-bound row updates do not all coincide
+    if (stagger > 0) {
+        const unsigned g = (blockIdx.x >> 3) & 3;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g * (unsigned)stagger) __builtin_amdgcn_s_sleep(10);
+    }
     constexpr int NR = G::NR;
     constexpr size_t MN = (size_t)MM * NN;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -652,14 +692,14 @@ bool has_shape(int M, int N) {
 
 int launch(int M, int N, size_t planes, hipStream_t s, const float* hty, float* sA, float* sB, float* traj,
            size_t traj_stride, float* x_out, const float* Ct, const float2* twM, const float2* twN, const float* prm,
-           int maxit) {
+           int maxit, int stagger) {
 #define X(m, n)                                                                                                  \
     if (M == m && N == n) {                                                                                      \
         constexpr size_t lds = Geo<m, n>::lds_bytes();                                                           \
         (void)hipFuncSetAttribute((const void*)resident_kernel<m, n>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                     \
         resident_kernel<m, n><<<dim3((unsigned)planes), kNT, lds, s>>>(hty, sA, sB, traj, traj_stride, x_out, Ct, \
-                                                                        twM, twN, prm, maxit);                   \
+                                                                        twM, twN, prm, maxit, stagger);          \
         return 0;                                                                                                \
     }
     RS_SHAPES(X)

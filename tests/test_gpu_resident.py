@@ -1,0 +1,102 @@
+"""GPU parity of the CU-resident solve for smooth non-power-of-two shapes (admm_resident.hip: one workgroup per
+plane runs all K iterations; the 2-pass smooth kernels of admm_smooth.hip are what it replaces).
+
+Oracle: oracle/oracle_np.py (restatement of /root/reference/src/ops/ops.jl:17-96, any M x N through FFTW at
+ops.jl:26,86; parity unpinned against Julia itself).  Tolerance: tests/parity.py (per-plane
+rel-L2 <= 1e-5, max-abs <= 2e-4 max|ref|).  Every case is also solved with ADMM_OPT_RESIDENT = 0 (the 2-pass
+kernels): two fp32 evaluations of the same algebra through different FFT factorisations, held to 1e-5."""
+import numpy as np
+import pytest
+import torch
+
+import admm_deconv
+import oracle_np
+from admm_deconv import _lib, synth
+from parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (B, P, N, M, psf, lam, rho, K) -- N lines of M pixels (Julia M x N)
+    (2, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 25),   # BASELINE's image side at 250
+    (1, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 1),    # K = 1: no update, straight to the last inverse
+    (1, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 2),    # one update: the chunk halos of the next spectra
+    (3, 1, 250, 250, None, 0.05, 0.1, 7),                      # no PSF (H^T y = y), stronger prox
+    (1, 3, 250, 250, ("rand", 9, 7), 0.01, 0.05, 5),           # RGB, asymmetric random PSF
+]
+
+
+def _psf(spec, rng):
+    if spec is None:
+        return None
+    if spec[0] == "gauss":
+        return synth.gaussian_psf(spec[1], spec[2])
+    h = rng.random((spec[2], spec[1])).astype(np.float32)
+    return (h / h.sum()).astype(np.float32)
+
+
+def _solve(dev, y, lam, rho, h, K, resident):
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    with _lib.option("RESIDENT", int(resident)):
+        x = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), lam, rho, ht, False, K)
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+def _resident_ran(dev, y, h, K):
+    """The resident kernel is one ADMM_K_PLANE launch (the 2-pass path launches column / line kernels)."""
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), 0.0041, 0.021, ht, False, K)
+    _lib.profile_enable(False)
+    names = {name: _lib.profile_get(cls)[1] for cls, name in _lib.KERNEL_CLASSES.items()}
+    return names.get("plane", 0) == 1 and names.get("column", 0) == 0
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}" for c in CASES])
+def test_resident_parity_vs_oracle_and_2pass(dev, case):
+    B, P, N, M, spec, lam, rho, K = case
+    rng = np.random.default_rng(N + 3 * M + K)
+    h = _psf(spec, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=11)
+    assert _resident_ran(dev, y, h, K), "the resident kernel did not run for this shape"
+    got = _solve(dev, y, lam, rho, h, K, True)
+    two = _solve(dev, y, lam, rho, h, K, False)
+    ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), np.float32(lam),
+                                                    np.float32(rho), oracle_np.psf_from_c(h), False, K))
+    assert_parity(got, ref, what="resident " + str(case))
+    d = np.linalg.norm((got - two).ravel()) / np.linalg.norm(two.ravel())
+    assert d < 1e-5, f"resident vs 2-pass rel-L2 {d:.2e}"
+
+
+def test_resident_deterministic_and_batch_invariant(dev):
+    h = synth.gaussian_psf(15, 2.5)
+    y = torch.from_numpy(synth.make_batch(6, 250, 250, h)).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    a = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 9)
+    b = admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, False, 9)
+    part = torch.cat([admm_deconv.tvd_fft(y[i:i + 2].contiguous(), 0.0041, 0.021, ht, False, 9) for i in (0, 2, 4)])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), "solve must be bitwise deterministic"
+    assert torch.equal(a, part), "planes are independent (ops.jl:168-173): sub-batches give the same planes"
+
+
+def test_resident_recorded_gradients_match_2pass(dev):
+    """Training at a smooth size: the recording forward runs resident (s_k into the trajectory slots), the
+    reverse sweep is the 2-pass adjoint.  Gradients against the all-2-pass recording within fp32 rounding."""
+    h = synth.gaussian_psf(9, 1.5)
+    yb = synth.make_batch(2, 250, 250, h, g0=3)
+    out = {}
+    for res in (1, 0):
+        with _lib.option("RESIDENT", res):
+            y = torch.from_numpy(yb).to(dev).requires_grad_(True)
+            lam = torch.tensor([0.0041], device=dev, requires_grad=True)
+            x = admm_deconv.tvd_fft(y, lam, 0.021, torch.from_numpy(h).to(dev), False, 6)
+            (x * x).sum().backward()
+            torch.cuda.synchronize()
+            out[res] = (x.detach().cpu().numpy(), y.grad.cpu().numpy(), float(lam.grad))
+    for i, what in ((0, "x"), (1, "y_bar")):
+        d = np.linalg.norm((out[1][i] - out[0][i]).ravel()) / np.linalg.norm(out[0][i].ravel())
+        assert d < 1e-5, f"{what}: resident recording vs 2-pass rel-L2 {d:.2e}"
+    assert abs(out[1][2] - out[0][2]) <= 1e-4 * abs(out[0][2]), (out[1][2], out[0][2])

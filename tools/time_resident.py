@@ -15,6 +15,13 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 import admm_deconv  # noqa: E402
 from admm_deconv import _lib, synth  # noqa: E402
 
+# NAME=VALUE arguments are library options (admm_set_option), e.g. PLANE_STAGGER=3500
+for _a in [a for a in sys.argv[1:] if "=" in a]:
+    _lib.set_option(_a.split("=")[0].upper(), int(_a.split("=")[1]))
+    sys.argv.remove(_a)
+TIME_ONLY = "--time-only" in sys.argv
+if TIME_ONLY:
+    sys.argv.remove("--time-only")
 SHAPES = [(250, 250, 256, 25)]
 if len(sys.argv) > 1:
     SHAPES = [tuple(int(v) for v in (a.split(",") + ["25"])[:4]) for a in sys.argv[1:]]
@@ -41,7 +48,7 @@ def main():
         hp = synth.gaussian_psf(15, 2.5)
         h = torch.from_numpy(hp).to(dev)
         # parity on 2 planes at a short K and the full K
-        for k_chk, with_h in ((3, True), (K, True), (4, False)):
+        for k_chk, with_h in (() if TIME_ONLY else ((3, True), (K, True), (4, False))):
             yb = synth.make_batch(2, M, N, hp if with_h else None)
             y = torch.from_numpy(yb).to(dev)
             hh = h if with_h else None
@@ -57,7 +64,7 @@ def main():
             out.append(r)
         y = torch.from_numpy(synth.make_batch(min(B, 8), M, N, hp)).to(dev)
         y = y.repeat((B + 7) // 8, 1, 1, 1)[:B].contiguous()
-        for res in (True, False):
+        for res in ((True,) if TIME_ONLY else (True, False)):
             for _ in range(2):
                 solve(y, h, K, res)
             reps = 5
