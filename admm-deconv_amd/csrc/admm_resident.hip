@@ -189,11 +189,13 @@ __device__ __forceinline__ void ipass(int cnt, const float2* __restrict__ tw, Ac
             for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tw, j * m * TS));
         }
     };
-    for (int i0 = tid(); i0 < total; i0 += 2 * kNT) {
+    // two butterflies in flight for small radices; one for R > 10 (register pressure next to the spectrum)
+    constexpr int U = R <= 10 ? 2 : 1;
+    for (int i0 = tid(); i0 < total; i0 += U * kNT) {
         const int i1 = i0 + kNT;
         int f0, b0, j0, f1 = 0, b1 = 0, j1 = 0;
         where(i0, f0, b0, j0);
-        const bool two = i1 < total;
+        const bool two = U == 2 && i1 < total;
         if (two) where(i1, f1, b1, j1);
         float2 v0[R], v1[R];
 #pragma unroll
@@ -363,10 +365,10 @@ __device__ __forceinline__ float2 lane_swap(float2 v) {   // value of lane t ^ 1
 }
 
 // Per-thread constants of the pair staging / separation (branch-free, so a register's store is one
-// ds_write at a compile-time offset from the thread's base)
+// ds_write at a compile-time offset from the thread's base).  At DC and Nyquist both lanes of a pair write
+// the same slot with the same value (the real parts of both lines).
 struct ZLane {
     int slot;        // z slot this lane writes: k (even line) or M - k (odd line)
-    bool wr;         // odd lanes skip DC and Nyquist (their z slot is the even lane's)
     float sgn;       // +1 even, -1 odd
     float im;        // 0 at DC / Nyquist (a real line's inverse keeps only the real parts), else 1
     bool odd;
@@ -374,7 +376,7 @@ struct ZLane {
 template <int MM>
 __device__ __forceinline__ ZLane zlane(int k, bool odd) {
     const bool edge = k == 0 || 2 * k == MM;
-    return {odd ? (edge ? k : MM - k) : k, !odd || !edge, odd ? -1.0f : 1.0f, edge ? 0.0f : 1.0f, odd};
+    return {odd ? (edge ? k : MM - k) : k, odd ? -1.0f : 1.0f, edge ? 0.0f : 1.0f, odd};
 }
 // own X_j(k) and the partner lane's X_{j^1}(k) -> z value: even line z[k] = X_2f + i X_2f+1,
 // odd line z[M - k] = conj X_2f + i conj X_2f+1 (Hermitian extension)
@@ -415,17 +417,17 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
             for (int r = jc0 / LS; r <= (jc1 - 1) / LS; ++r) {
                 const int j = r * LS + th.jt;
                 const float2 z = zval(S[r], lane_swap(S[r]), zl);
-                if (zl.wr && (r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1))
+                if ((r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1))
                     zb[((r * LS - jc0) / 2 + HP) * MM] = z;
             }
             if constexpr (HP) {
                 constexpr int hA = (jc0 + NN - 2) % NN, hB = jc1 % NN;   // even lines: pairs (hA, hA+1), (hB, hB+1)
                 const float2 sA = C >= 1 ? hs[C] : S[hA / LS];
                 const float2 zA = zval(sA, lane_swap(sA), zl);
-                if (zl.wr && (th.jt >> 1) == (hA % LS) / 2) buf[zl.slot] = zA;
+                if ((th.jt >> 1) == (hA % LS) / 2) buf[zl.slot] = zA;
                 const float2 sB = (C == G::NLC - 1 && G::NLC > 1) ? hs[0] : S[hB / LS];
                 const float2 zB = zval(sB, lane_swap(sB), zl);
-                if (zl.wr && (th.jt >> 1) == (hB % LS) / 2) buf[(NP - 1) * MM + zl.slot] = zB;
+                if ((th.jt >> 1) == (hB % LS) / 2) buf[(NP - 1) * MM + zl.slot] = zB;
             }
         }
         __syncthreads();
@@ -456,15 +458,13 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
         const float tau = a.tau, rho = a.rho;
         const rsrc_t rso = make_rsrc(a.so, 2 * MN * 4), rsn = make_rsrc(a.sn, 2 * MN * 4), rh = make_rsrc(a.hty, MN * 4);
         // float offsets of pixel i and its neighbours within a pair row (LDS), byte offset of i + 1 (HBM)
-        int pc[QN], pl[QN], pr[QN];
-        unsigned gr[QN];
+        // (left and right neighbour offsets packed in one register: 16 bits each)
+        int pc[QN], plr[QN];
 #pragma unroll
         for (int q = 0; q < QN; ++q) {
             const int i = lane + 64 * q < MM ? lane + 64 * q : 0;
             pc[q] = 2 * dpos<MM>(i);
-            pl[q] = 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1);
-            pr[q] = 2 * dpos<MM>(i + 1 == MM ? 0 : i + 1);
-            gr[q] = 4u * (unsigned)(i + 1 == MM ? 0 : i + 1);
+            plr[q] = 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1) | (2 * dpos<MM>(i + 1 == MM ? 0 : i + 1)) << 16;
         }
         const unsigned gl = 4u * (unsigned)lane;   // + 256 q: the instruction's immediate offset
         auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
@@ -489,7 +489,7 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                 }
             }
             struct GIn {
-                float a0n, a1, a1r, h;
+                float a0n, a1, h;
             };
             auto gload = [&](GIn (&g)[QN], int u) {
                 const int j = jc0 + u - 2;
@@ -501,9 +501,8 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                     if (!a.first) {
                         g[q].a0n = bld1(rso, gl + 256 * q, on);
                         g[q].a1 = bld1(rso, gl + 256 * q, oj + 4 * MN);
-                        g[q].a1r = bld1(rso, gr[q], oj + 4 * MN);
                     } else {
-                        g[q].a0n = g[q].a1 = g[q].a1r = 0.0f;
+                        g[q].a0n = g[q].a1 = 0.0f;
                     }
                 }
             };
@@ -528,8 +527,23 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                 for (int q = 0; q < QN; ++q) {
                     xcq[q] = Xf[ru + pc[q]];
                     xnq[q] = Xf[rn + pc[q]];
-                    xlq[q] = Xf[ru + pl[q]];
-                    xrq[q] = Xf[ru + pr[q]];
+                    xlq[q] = Xf[ru + (plr[q] & 0xffff)];
+                    xrq[q] = Xf[ru + (plr[q] >> 16)];
+                }
+                // s_old channel 1 of pixel i + 1: the next lane's (lane 63: lane 0 of the next slice; the
+                // last pixel wraps to pixel 0), through ds_bpermute instead of a second load
+                float a1r[QN];
+                {
+                    float sh[QN];
+#pragma unroll
+                    for (int q = 0; q < QN; ++q)
+                        sh[q] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * ((lane + 1) & 63), __float_as_int(cur[q].a1)));
+                    const float p0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cur[0].a1)));
+#pragma unroll
+                    for (int q = 0; q < QN; ++q) {
+                        const float nx1 = q + 1 < QN ? sh[q + 1 < QN ? q + 1 : q] : p0;
+                        a1r[q] = lane + 64 * q + 1 == MM ? p0 : (lane == 63 ? nx1 : sh[q]);
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < QN; ++q) {
@@ -542,7 +556,7 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
                         bst1(rsn, gl + 256 * q, oj + 4 * MN, s1);
                     }
                     const float w1 = prox_w(s1, tau);
-                    const float w1r = prox_w((xr - xc) + clipf(cur[q].a1r, tau), tau);
+                    const float w1r = prox_w((xr - xc) + clipf(a1r[q], tau), tau);
                     const float v = fmaf(rho, (w0c[q] - w0n) + (w1 - w1r), cur[q].h);
                     w0c[q] = w0n;
                     if (u == ua) vf[q] = v;
@@ -677,7 +691,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 // ---- host side -----------------------------------------------------------------------------------------------
 // Shapes compiled here (M = line length, N = lines): square smooth sides the 2-pass path serves
 #ifndef RS_SHAPES_OVERRIDE
-#define RS_SHAPES(X) X(250, 250)
+#define RS_SHAPES(X) X(250, 250) X(240, 240) X(200, 200) X(192, 192) X(160, 160) X(120, 120) X(96, 96)
 #else
 #define RS_SHAPES(X) RS_SHAPES_OVERRIDE(X)
 #endif
