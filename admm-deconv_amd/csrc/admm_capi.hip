@@ -640,7 +640,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     // CU-resident solve (admm_resident.hip): anisotropic, no dim-2 spectra or isotropic norms recorded; it
     // forms the first line spectrum itself, so PREP only produces H^T y
     const bool res = !iso && !tr.v && !tr.nrm && !tr.m && opt(ADMM_OPT_RESIDENT) != 0 && opt(ADMM_OPT_SMOOTH) != 0 &&
-                     admm::rs::has_shape(M, N);
+                     admm::rs::has_shape(M, N, opt(ADMM_OPT_RESIDENT) >= 2);
     // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
     if (!res || kh > 0) {
         rc = line_fwd(y, spec0);

@@ -696,7 +696,15 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #define RS_SHAPES(X) RS_SHAPES_OVERRIDE(X)
 #endif
 
-bool has_shape(int M, int N) {
+// Compiled shapes where the 2-pass smooth kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the
+// 2-pass path; 2 forces the resident kernel on every compiled shape)
+#define RS_SLOWER(X)
+
+bool has_shape(int M, int N, bool all) {
+#define X(m, n) \
+    if (!all && M == m && N == n) return false;
+    RS_SLOWER(X)
+#undef X
 #define X(m, n) \
     if (M == m && N == n) return true;
     RS_SHAPES(X)

@@ -9,8 +9,9 @@
 namespace admm {
 namespace rs {
 
-// M = line length (contiguous), N = lines; true if this build has a resident kernel for M x N
-bool has_shape(int M, int N);
+// M = line length (contiguous), N = lines; true if this build has a resident kernel for M x N (all = false:
+// only where it measured faster than the 2-pass kernels)
+bool has_shape(int M, int N, bool all = false);
 // hty: H^T y per plane (or y itself without a PSF); s ping-pong buffers sA / sB ([plane][2][N][M]) unless
 // traj != nullptr (then s_k goes to traj + (k - 1) * traj_stride, read back from the previous slot);
 // Ct / twM / twN / prm: the setup kernel's tables; stagger: start delay per workgroup group (realtime ticks,

@@ -237,8 +237,9 @@ enum {
                                     lengths (admm_smooth.hip); 0: runtime plans for every such shape;
                                     2 / 3: compiled, column plans forced increasing / decreasing (sweeps)  */
     ADMM_OPT_RESIDENT = 8,       /* 1 (default): one workgroup per plane runs all K iterations for the smooth
-                                    non-power-of-two shapes admm_resident.hip compiled (anisotropic, no h_bar
-                                    trajectory); 0: the 2-pass smooth kernels                                 */
+                                    non-power-of-two shapes admm_resident.hip compiled and measured faster
+                                    (anisotropic, no h_bar trajectory); 2: every compiled shape; 0: the
+                                    2-pass smooth kernels                                                     */
     ADMM_OPT_COUNT = 9
 };
 int admm_set_option(int option, int value);

@@ -23,6 +23,12 @@ CASES = [
     (1, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 2),    # one update: the chunk halos of the next spectra
     (3, 1, 250, 250, None, 0.05, 0.1, 7),                      # no PSF (H^T y = y), stronger prox
     (1, 3, 250, 250, ("rand", 9, 7), 0.01, 0.05, 5),           # RGB, asymmetric random PSF
+    (2, 1, 240, 240, ("gauss", 15, 2.5), 0.0041, 0.021, 9),    # 240 = 15 x 16 both ways (forced: RESIDENT = 2)
+    (2, 1, 200, 200, ("gauss", 9, 1.5), 0.0041, 0.021, 9),
+    (2, 1, 192, 192, ("rand", 10, 10), 0.02, 0.1, 6),         # 3 pixel slices per lane in the update
+    (2, 1, 160, 160, None, 0.05, 0.1, 6),
+    (3, 1, 120, 120, ("gauss", 15, 2.5), 0.0041, 0.021, 8),    # one line chunk: halo pairs are its own lines
+    (4, 1, 96, 96, ("gauss", 9, 1.5), 0.0041, 0.021, 25),
 ]
 
 
@@ -37,7 +43,7 @@ def _psf(spec, rng):
 
 def _solve(dev, y, lam, rho, h, K, resident):
     ht = None if h is None else torch.from_numpy(h).to(dev)
-    with _lib.option("RESIDENT", int(resident)):
+    with _lib.option("RESIDENT", 2 * int(resident)):   # 2: every compiled shape, even where 2-pass is faster
         x = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), lam, rho, ht, False, K)
     torch.cuda.synchronize()
     return x.cpu().numpy()
@@ -48,7 +54,8 @@ def _resident_ran(dev, y, h, K):
     ht = None if h is None else torch.from_numpy(h).to(dev)
     _lib.profile_reset()
     _lib.profile_enable(True)
-    admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), 0.0041, 0.021, ht, False, K)
+    with _lib.option("RESIDENT", 2):
+        admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), 0.0041, 0.021, ht, False, K)
     _lib.profile_enable(False)
     names = {name: _lib.profile_get(cls)[1] for cls, name in _lib.KERNEL_CLASSES.items()}
     return names.get("plane", 0) == 1 and names.get("column", 0) == 0
