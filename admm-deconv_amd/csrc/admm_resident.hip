@@ -595,6 +595,8 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
         dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, al);
     }
     // ---- half spectra separated into S: X_2f = (z + conj z(-k)) / 2, X_2f+1 = (z - conj z(-k)) / (2i) ----
+    // (Only the threads that hold spectrum bins.  Reading into every thread's registers unconditionally, so
+    // that the chunk's old registers die early, measured 68k vs 78k img/s at 250^2: more scratch, not less.)
     if (th.act) {
         const int k = th.k, km = k == 0 ? 0 : MM - k;
         const bool odd = th.jt & 1;
@@ -698,7 +700,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 
 // Compiled shapes where the 2-pass smooth kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the
 // 2-pass path; 2 forces the resident kernel on every compiled shape)
-#define RS_SLOWER(X)
+#define RS_SLOWER(X) X(240, 240)
 
 bool has_shape(int M, int N, bool all) {
 #define X(m, n) \
