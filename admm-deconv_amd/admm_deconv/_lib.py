@@ -38,7 +38,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
-           "admm_tvd_backward_multi_recorded_dev_f32")
+           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async")
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
 REC_HBAR, REC_MASKS = 1, 2
@@ -146,6 +146,8 @@ def load():
     L.admm_profile_reset.argtypes = []
     L.admm_profile_get.restype = c_int
     L.admm_profile_get.argtypes = [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+    L.admm_copy_async.restype = c_int
+    L.admm_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
     _lib = L
     return L
 
@@ -175,6 +177,11 @@ def multi_workspace_bytes(M, N, P, B, nbranch, maxit, flags):
     out = ctypes.c_size_t(0)
     check(load().admm_tvd_multi_workspace_bytes(M, N, P, B, nbranch, int(maxit), int(flags), ctypes.byref(out)))
     return out.value
+
+
+def copy_async(dst, src, nbytes, stream):
+    """admm_copy_async: hipMemcpyAsync of nbytes between device pointers on a HIP stream handle (int)."""
+    check(load().admm_copy_async(dst, src, nbytes, stream))
 
 
 def profile_enable(on=True):

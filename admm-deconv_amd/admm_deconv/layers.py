@@ -213,8 +213,9 @@ class Parallel:
     When every branch is an ADMM layer the one-grid solve covers (the denoiser: ADMMDeconvF2((), K, ρ_i, σ),
     256 x 256, same K and prox; isotropic only with merge="always" and no ρ needing a gradient), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
     planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
-    each branch's bias and σ then apply to its slice.  Results are bitwise those of the branches run one
-    by one.  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
+    each branch's bias and σ then apply to its slice.  The forward output, λ̄ and ρ̄ are bitwise those of the
+    branches run one by one; the input gradient matches them to fp32 rounding (branch_sum_kernel adds the
+    branches' ȳ in a fixed order, not in autograd's per-branch accumulation order).  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
     (forward, and -- autograd replays a backward op on its forward's stream -- the adjoint too), then the
     caller's stream waits for all of them.  merge=False keeps the per-branch path; streams=False runs the
     branches one after the other on the caller's stream (the reference's single task-local stream)."""

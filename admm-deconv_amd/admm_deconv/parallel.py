@@ -17,6 +17,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import _lib
+
 __all__ = ["shard_range", "solve_sharded", "ShardGather"]
 
 
@@ -66,7 +68,11 @@ class ShardGather:
     `gathered()` returns rank dst's (world * B_local, ...) result of the last step (None elsewhere).  It is
     a collective (every rank calls it): it makes the device work of every rank complete and, for "ipc",
     runs a barrier, so the peer writes into rank dst's buffer have landed.  The receive side is double
-    buffered by step parity: the returned tensor stays valid until two more steps have been issued.
+    buffered by step parity: the returned tensor stays valid until two more steps have been issued -- on
+    EVERY rank.  step() itself does not synchronise the ranks, so with engine "ipc" a peer that runs two
+    steps ahead of rank dst would overwrite the buffer rank dst is still reading.  A caller that consumes the
+    gathered batch therefore calls gathered() (collectively) after every step it consumes; a caller that
+    only streams steps (the benchmark) never reads the buffers in between.
 
     engine="ipc" moves the outputs without any collective kernel: rank dst shares its receive buffer
     once through a HIP IPC handle, and every rank copies each solved slice into its part of it with an
@@ -103,7 +109,7 @@ class ShardGather:
         else:
             self.recv = None
         if self.async_comm:
-            self.comm = torch.cuda.Stream(device=y_local.device)
+            self.comm = getattr(self, "comm", None) or torch.cuda.Stream(device=y_local.device)
             self.freed = [None, None]      # event: the gathers reading out[b] have completed
         self.i = 0
 
@@ -132,8 +138,9 @@ class ShardGather:
                     raise RuntimeError("shape mismatch")
                 # one real copy through the path the steps use (peer access, engine choice): any error
                 # here selects RCCL instead of failing mid-run; the slice is overwritten by the first step
+                self.comm = torch.cuda.Stream(device=y_local.device)
                 for r in self.remote:
-                    r[self.rank * n: self.rank * n + 1].copy_(y_local[:1])
+                    self._push(r, y_local, 0, 1)
                 torch.cuda.synchronize(y_local.device)
         except Exception:   # noqa: BLE001
             ok = 0
@@ -160,6 +167,19 @@ class ShardGather:
         s, k = self.bounds[c]
         return [self.recv[b][r * n + s: r * n + s + k] for r in range(self.world)]
 
+    def _push(self, remote, out, s, k):
+        """Copy this rank's solved slice [s, s + k) into its part of rank dst's IPC-opened receive buffer, on the
+        comm stream.  An explicit hipMemcpyAsync through the library (admm_copy_async), not Tensor.copy_: a
+        cross-device copy_ also synchronises with the current stream of the PEER device, which would make this
+        process create and use a queue on rank dst's GPU.  The runtime gives device-to-device copies between
+        GPUs of >= ROC_P2P_SDMA_SIZE (1 MiB default; a c3 slice is 64 MiB / chunks) to an SDMA engine."""
+        n = self.y.shape[0]
+        dst = remote[self.rank * n + s: self.rank * n + s + k]
+        src = out[s:s + k]
+        assert dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype and dst.shape == src.shape
+        src.record_stream(self.comm)
+        _lib.copy_async(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), self.comm.cuda_stream)
+
     def step(self):
         b = self.i & 1
         out = self._out(b)
@@ -175,8 +195,7 @@ class ShardGather:
                 with torch.cuda.stream(self.comm):
                     self.comm.wait_event(done)
                     if self.engine == "ipc":
-                        n = self.y.shape[0]
-                        self.remote[b][self.rank * n + s: self.rank * n + s + k].copy_(out[s:s + k], non_blocking=True)
+                        self._push(self.remote[b], out, s, k)
                     else:
                         dist.gather(out[s:s + k], self._parts(c, b), dst=self.dst, group=self.group)
             else:

@@ -1767,6 +1767,14 @@ int admm_profile_get(int kernel_class, double* total_ms, long long* launches) {
     return ADMM_OK;
 }
 
+int admm_copy_async(void* dst, const void* src, size_t bytes, void* stream) {
+    if (bytes == 0) return ADMM_OK;
+    if (!dst || !src) return fail(ADMM_E_INVALID, "admm_copy_async: NULL pointer");
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_copy_async: %s", hipGetErrorString(e));
+    return ADMM_OK;
+}
+
 int admm_tvd_multi_workspace_bytes(int M, int N, int P, int B, int nbranch, int maxit, int flags, size_t* out_bytes) {
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_multi(M, N, P, B, nbranch, maxit, flags);

@@ -166,8 +166,11 @@ template <bool PSF>
 __global__ __launch_bounds__(kPT) void plane256_iso_kernel(const float* __restrict__ y, float* __restrict__ x_out,
                                                            const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                            const float2* __restrict__ Gf, const float2* __restrict__ G0b,
-                                                           float2* __restrict__ hln, const float4* __restrict__ s_in,
-                                                           float4* __restrict__ s_out, const float2* __restrict__ fmap,
+                                                           float2* __restrict__ hln,
+                                                           // s_in == s_out (in place) when no trajectory is
+                                                           // recorded, so neither is __restrict__
+                                                           const float4* s_in, float4* s_out,
+                                                           const float2* __restrict__ fmap,
                                                            float2* __restrict__ qpart, const float* __restrict__ prm,
                                                            int k, int K, Branches br) {
     const BranchOf bo = branch_of(br, blockIdx.x);

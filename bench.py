@@ -399,28 +399,60 @@ def main():
         else:
             solve(y, out)
 
+    def timed(body, steps):
+        """Barrier + synchronize on both sides of `steps` calls of body; (this rank's seconds, max over ranks,
+        ms from this rank's last solve being enqueued to the end of its device work)."""
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            body()
+        solved = torch.cuda.Event(enable_timing=True)
+        solved.record(stream)                # after the last solve on the compute stream
+        if sg is not None:
+            sg.wait()                        # the compute stream waits for this rank's gathers / peer copies
+        done = torch.cuda.Event(enable_timing=True)
+        done.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        mx = el
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            mx = float(t.item())
+        return el, mx, solved.elapsed_time(done)
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if sg is not None:
-        sg.wait()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el_rank, el, tail_ms = timed(step, args.steps)
     images = B * world * args.steps
     value = images / el
     ms_per_step = 1000.0 * el / max(args.steps, 1)
+
+    ranks = None
+    solve_only = None
+    if world > 1:
+        # diagnostics for the multi-GPU record (outside the timed region above): the same steps solve-only (no
+        # gather) in this invocation, and per rank what it saw -- which engine ran, how long its own steps took,
+        # how long its gathers ran past its last solve, and which device it drove
+        so_rank, so_el, _ = timed(lambda: solve(y, out), args.steps) if gather else (el_rank, el, 0.0)
+        props = torch.cuda.get_device_properties(dev)
+        me = {"rank": rank, "world_seen": dist.get_world_size(), "backend": dist.get_backend(),
+              "device": dev.index, "visible_devices": torch.cuda.device_count(),
+              "device_uuid": str(getattr(props, "uuid", "")), "pci_bus_id": getattr(props, "pci_bus_id", None),
+              "gather_engine": (sg.engine if sg is not None else None),
+              "ms_per_step": round(1000.0 * el_rank / args.steps, 4),
+              "solve_only_ms_per_step": round(1000.0 * so_rank / args.steps, 4),
+              "gather_tail_ms": round(tail_ms, 4)}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        solve_only = {"ms_per_step": round(1000.0 * so_el / args.steps, 4),
+                      "value": round(images / so_el, 2),
+                      "note": "same steps and shards without the gather, max over ranks (not the metric)"}
 
     # ---- per-kernel timing (separate instrumented solve; not part of the timed region) ----
     _lib.profile_reset()
@@ -486,6 +518,9 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
         }
+        if ranks is not None:
+            line["ranks"] = ranks
+            line["solve_only"] = solve_only
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -150,9 +150,12 @@ int admm_tvd_backward_sharded_f32(const float* y, const float* x_bar, float* y_b
  *       256 x 256 anisotropic reverse sweep, 8 of its 24 B/px per step gone.  lambda_bar, y_bar and h_bar
  *       are bitwise those of a full recording; a replay with rho_bar != NULL fails with ADMM_E_INVALID.
  *       Honoured by the fused anisotropic trajectory (256 x 256, no h_bar); isotropic at 256 x 256 (no
- *       h_bar, no reducer) it selects the fused isotropic sweep instead (plane_iso.hip: s_k and |s_k| kept
- *       in the kernels' lane-native layout, no rho_bar either); elsewhere the full trajectory is recorded
- *       and rho_bar stays available. */
+ *       h_bar) it selects the fused isotropic sweep instead (plane_iso.hip: s_k and |s_k| kept in the
+ *       kernels' lane-native layout, no rho_bar either), also for a sharded batch: the reducer then sums
+ *       the R map of every reverse step over the shards before s_bar is formed, while lambda_bar is this
+ *       shard's partial (tau_bar from the shard's own R), so the caller sums lambda_bar over the shards as
+ *       it does for the 2-pass sweep; elsewhere the full trajectory is recorded and rho_bar stays
+ *       available. */
 enum { ADMM_REC_HBAR = 1, ADMM_REC_MASKS = 2 };
 
 int admm_tvd_forward_record_f32(const float* y, float* x_out, int M, int N, int P, int B,
@@ -244,6 +247,14 @@ enum {
 };
 int admm_set_option(int option, int value);
 int admm_get_option(int option, int* value);
+
+/* Output transport of the batch-sharded solve (BASELINE c3; the reference gathers nothing -- its batch
+ * lives on one device, ops.jl:168-173): an asynchronous copy of `bytes` from src to dst on `stream`, both
+ * device pointers, dst possibly memory of another GPU opened through a HIP IPC handle.  A plain
+ * hipMemcpyAsync on the caller's stream: the runtime gives device-to-device copies between GPUs of at
+ * least ROC_P2P_SDMA_SIZE (1 MiB by default) to an SDMA engine, so the transfer holds no CU and touches
+ * no HIP stream of the peer device.  ADMM_E_INVALID for NULL pointers, ADMM_E_HIP if the runtime refuses. */
+int admm_copy_async(void* dst, const void* src, size_t bytes, void* stream);
 
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises

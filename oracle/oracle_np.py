@@ -25,7 +25,7 @@ import numpy as np
 
 __all__ = [
     "from_c", "to_c", "psf_from_c", "ST", "BT", "pixelnorm", "make_C",
-    "D_op", "Dt_op", "H_op", "Ht_op", "tvd_fft_literal", "tvd_fft_spectral", "tvd_fft",
+    "D_op", "Dt_op", "H_op", "Ht_op", "prox_active_fraction", "tvd_fft_literal", "tvd_fft_spectral", "tvd_fft",
 ]
 
 
@@ -167,10 +167,25 @@ def _check(y, lam, rho, maxit):
     return np.asarray(y, dtype=np.float64)
 
 
-def tvd_fft_literal(y, lam, rho, h=None, isotropic=False, maxit=100):
+def _record_prox(stats, z, maxit, k):
+    """stats['prox_active'][k] = fraction of non-zero prox outputs z_k (ST/BT, ops.jl:89).  The K-th
+    iteration's z is dead (ops.jl:84-93), so only iterations 1..K-1 are recorded: a case whose fractions are
+    all 0 exercises only the linear part of the solve."""
+    if stats is not None and k < maxit - 1:
+        stats.setdefault("prox_active", []).append(float(np.count_nonzero(z)) / z.size)
+
+
+def prox_active_fraction(stats):
+    """Mean fraction of live prox outputs over the iterations that reach the output (0 when none do)."""
+    a = stats.get("prox_active", [])
+    return float(np.mean(a)) if a else 0.0
+
+
+def tvd_fft_literal(y, lam, rho, h=None, isotropic=False, maxit=100, stats=None):
     """Op-for-op restatement of ops.jl:17-96 in fp64 (spatial stencils, spatial H^T).
 
     y: (M,N,P,B) Julia-order array; lam, rho: scalars; h: (kh,kw) PSF or None/empty.
+    stats: optional dict, filled by _record_prox.
     Returns x of shape (M,N,P,B) float64."""
     y = _check(y, lam, rho, maxit)
     M, N, P, B = y.shape
@@ -187,15 +202,16 @@ def tvd_fft_literal(y, lam, rho, h=None, isotropic=False, maxit=100):
     # H^T(y) is loop-invariant; the reference re-evaluates it every iteration (ops.jl:86)
     # and gets the identical array each time, so evaluating it once is exact.
     hty = yp.copy() if hj is None else Ht_op(yp, hj)
-    for _ in range(maxit):                                       # ops.jl:84-92
+    for k in range(maxit):                                       # ops.jl:84-92
         x = _irfft12(C * _rfft12(hty + rho * Dt_op(z - u)), M, N)
         Dxk = D_op(x)
         z = thresh(Dxk + u, tau)
+        _record_prox(stats, z, maxit, k)
         u = u + Dxk - z
     return x.transpose(0, 1, 3, 2)                               # ops.jl:93
 
 
-def tvd_fft_spectral(y, lam, rho, h=None, isotropic=False, maxit=100):
+def tvd_fft_spectral(y, lam, rho, h=None, isotropic=False, maxit=100, stats=None):
     """Independent form: D, D^T and H^T applied as Fourier multipliers (cross-check)."""
     y = _check(y, lam, rho, maxit)
     M, N, P, B = y.shape
@@ -232,7 +248,7 @@ def tvd_fft_spectral(y, lam, rho, h=None, isotropic=False, maxit=100):
     z = np.zeros((M, N, 2 * Bsz, P))
     u = np.zeros((M, N, 2 * Bsz, P))
     x = np.zeros((M, N, Bsz, P))
-    for _ in range(maxit):
+    for k in range(maxit):
         w = z - u
         W1 = _rfft12(w[:, :, 0::2, :])
         W2 = _rfft12(w[:, :, 1::2, :])
@@ -243,6 +259,7 @@ def tvd_fft_spectral(y, lam, rho, h=None, isotropic=False, maxit=100):
         Dx[:, :, 0::2, :] = _irfft12(L1 * X, M, N)
         Dx[:, :, 1::2, :] = _irfft12(L2 * X, M, N)
         z = thresh(Dx + u, tau)
+        _record_prox(stats, z, maxit, k)
         u = u + Dx - z
     return x.transpose(0, 1, 3, 2)
 

@@ -4,6 +4,35 @@ import numpy as np
 
 REL_L2_TOL = 1e-5
 MAXABS_TOL = 2e-4
+# a parity case pins the nonlinear part of the solve (ST/BT, /root/reference/src/ops/ops.jl:6-10, 89) only if
+# the prox is live: at least this fraction of the oracle's prox outputs z_k (or, adjoint, of the recorded
+# masks 1[|s_k| > tau]) must be non-zero, averaged over the iterations that reach the output
+PROX_MIN_FRACTION = 0.01
+
+
+def assert_prox_active(frac, what="", linear_only=False):
+    """Every parity case either proves that its prox fired (frac >= PROX_MIN_FRACTION) or is declared a
+    linear-only check (K = 1, tau above every |Dx|): then the prox must really be dead, so that the label
+    cannot hide a case that was meant to be nonlinear."""
+    if linear_only:
+        assert frac == 0.0, f"{what}: declared linear-only but {frac:.3%} of prox outputs are live"
+    else:
+        assert frac >= PROX_MIN_FRACTION, (f"{what}: prox live in only {frac:.3%} of elements "
+                                           f"(< {PROX_MIN_FRACTION:.0%}): the case checks only the linear solve")
+    return frac
+
+
+def oracle_solve(y, lam, rho, h, iso, K, form="literal", linear_only=False, what=""):
+    """The fp64 oracle (oracle/oracle_np.py) on C-layout fp32 inputs y (B,P,N,M), h (kw,kh) or None, with lam and
+    rho rounded to fp32 as the library takes them; asserts whether the prox fired (assert_prox_active)."""
+    import oracle_np
+    f = oracle_np.tvd_fft_literal if form == "literal" else oracle_np.tvd_fft_spectral
+    st = {}
+    x = oracle_np.to_c(f(oracle_np.from_c(np.asarray(y, np.float64)), np.float32(lam), np.float32(rho),
+                         oracle_np.psf_from_c(h), iso, K, stats=st))
+    if linear_only is not None:
+        assert_prox_active(oracle_np.prox_active_fraction(st), what, linear_only)
+    return x
 
 
 def assert_parity(got, ref, rel_tol=REL_L2_TOL, maxabs_tol=MAXABS_TOL, what=""):
@@ -24,3 +53,14 @@ def assert_parity(got, ref, rel_tol=REL_L2_TOL, maxabs_tol=MAXABS_TOL, what=""):
     mx = np.abs(got - ref).max() / scale
     assert mx <= maxabs_tol, f"{what}: max-abs {mx:.3e} > {maxabs_tol:.0e} * max|ref|"
     return worst, mx
+
+
+def assert_case_prox_active(y, lam, rho, h, iso, K, what="", linear_only=None):
+    """assert_prox_active for a case checked against another oracle form (the autograd gradient oracle): the
+    fraction comes from the fp64 spectral oracle's forward on the same inputs.  linear_only defaults to K == 1
+    (the K-th prox output is dead, ops.jl:84-93)."""
+    import oracle_np
+    st = {}
+    oracle_np.tvd_fft_spectral(oracle_np.from_c(np.asarray(y, np.float64)), np.float32(lam), np.float32(rho),
+                               oracle_np.psf_from_c(h), iso, K, stats=st)
+    return assert_prox_active(oracle_np.prox_active_fraction(st), what, K <= 1 if linear_only is None else linear_only)

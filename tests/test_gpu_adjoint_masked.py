@@ -33,6 +33,7 @@ import admm_deconv
 import oracle_torch
 from admm_deconv import _lib, synth
 from conftest import PKG_DIR, REPO
+from parity import assert_prox_active
 
 pytestmark = pytest.mark.gpu
 
@@ -57,10 +58,17 @@ CASES = [
     ("iso-256-c2-K25", 2, 1, 256, 256, ("gauss", 15, 2.5), 0.0041, 0.021, 25, True, True, {}),
     ("iso-256-c5layer-K50", 2, 3, 256, 256, None, 0.0041, 0.021, 50, True, False, {}),
     ("iso-generic-45x36-K6", 3, 1, 45, 36, ("gauss", 5, 1.0), 0.02, 0.1, 6, True, True, {}),
-    # the reference demo's shape (src/ADMM_Deconv.jl:17-23): 32x32x3x2, a 32x32 PSF, K = 50
+    # the reference demo's shape (src/ADMM_Deconv.jl:17-23): 32x32x3x2, a 32x32 PSF, K = 50.  The PSF as large as
+    # the image flattens it (|Dx| < 0.06): at tau = 0.05 / 0.3 the prox never fires (linear-only, lambda_bar = 0),
+    # at 0.0005 / 0.3 it is live in ~4 % of the elements, at 0.0002 / 0.3 in ~40-60 %
     ("demo-32-psf32-K50", 2, 3, 32, 32, ("rand", 32, 32), 0.05, 0.3, 50, False, True, {}),
+    ("demo-32-psf32-K50-live", 2, 3, 32, 32, ("rand", 32, 32), 0.0005, 0.3, 50, False, True, {}),
+    ("demo-32-psf32-K50-live59", 2, 3, 32, 32, ("rand", 32, 32), 0.0002, 0.3, 50, False, True, {}),
     ("generic-40x30-psf40x30-K9", 2, 1, 30, 40, ("rand", 40, 30), 0.02, 0.1, 9, False, True, {}),
+    ("generic-40x30-psf40x30-K9-live", 2, 1, 30, 40, ("rand", 40, 30), 0.0002, 0.3, 9, False, True, {}),
 ]
+# cases whose prox never fires (asserted on the recorded masks): they pin the linear part of the adjoint only
+LINEAR_ONLY = {"2pass-16x32-K1", "demo-32-psf32-K50", "generic-40x30-psf40x30-K9", "isofused-256-K1"}
 
 
 def _psf(spec, rng):
@@ -138,6 +146,13 @@ def _scalar_rel(a, b):
     return abs(a - b) / max(abs(b), 1e-300)
 
 
+def mask_fraction(masks):
+    """Mean fraction of live prox branches 1[|s_k| > tau] (iso: 1[||s_k|| > tau]) over the recorded iterations."""
+    if not masks:
+        return 0.0
+    return float(np.mean([np.mean(m if not isinstance(m, tuple) else m[0]) for m in masks]))
+
+
 def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned=False, need_rho=True):
     """GPU record + replay, the trajectory's masks, and the errors against the mask-conditioned fp64 oracle
     (and, as the arithmetic reference, of an fp32 torch evaluation of the same mask-conditioned computation)."""
@@ -158,6 +173,8 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
         if K > 1:
             s_traj, nrm = read_trajectory(rec, K, lane_native)
             masks = oracle_torch.masks_from_trajectory(s_traj, lam, rho, iso, nrm)
+        # the case must exercise the nonlinear reverse sweep (or be declared linear-only, and be so)
+        frac = assert_prox_active(mask_fraction(masks), cid, cid in LINEAR_ONLY)
         yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt, need_rho=need_rho)
         torch.cuda.synchronize()
     lam32, rho32 = np.float32(lam), np.float32(rho)
@@ -185,7 +202,11 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     if hb is not None:
         err["h_bar"] = _rel(hb.cpu().numpy(), hb0)
         ref32["h_bar"] = _rel(hb32, hb0)
-    info = {"rho_bar": rb0, "rho_bar_scale": rho_scale, "lambda_bar": lb0, "lambda_bar_scale": lam_scale,
+    if cid not in LINEAR_ONLY:
+        # tau enters the output only through live prox branches: a live case has lambda_bar != 0 on both sides
+        assert lb0 != 0.0 and float(lb) != 0.0, f"{cid}: lambda_bar is zero with {frac:.2%} of the prox live"
+    info = {"prox_live_fraction": frac,
+            "rho_bar": rb0, "rho_bar_scale": rho_scale, "lambda_bar": lb0, "lambda_bar_scale": lam_scale,
             "rel_to_value": {"lambda_bar": _scalar_rel(float(lb), lb0),
                              "rho_bar": _scalar_rel(float(rb), rb0) if need_rho else None}}
     if K > 1:

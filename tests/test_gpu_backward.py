@@ -22,7 +22,7 @@ import torch
 import admm_deconv
 import oracle_torch
 from admm_deconv import _lib, synth
-from parity import assert_parity
+from parity import assert_case_prox_active, assert_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -84,6 +84,7 @@ def test_backward_vs_autograd(dev, case):
     h = psf(spec, rng)
     y = synth.make_batch(B, M, N, h, P=P, g0=11)
     xbar = rng.standard_normal(y.shape).astype(np.float32)
+    assert_case_prox_active(y, lam, rho, h, False, K, str(case))
     ht = None if h is None else torch.from_numpy(h).to(dev)
     x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev),
                                                      lam, rho, ht, False, K)
@@ -124,6 +125,7 @@ def test_backward_iso_vs_autograd(dev, case):
     h = psf(spec, rng)
     y = synth.make_batch(B, M, N, h, P=P, g0=5)
     xbar = rng.standard_normal(y.shape).astype(np.float32)
+    assert_case_prox_active(y, lam, rho, h, True, K, "iso " + str(case))
     ht = None if h is None else torch.from_numpy(h).to(dev)
     x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev),
                                                      lam, rho, ht, True, K)
@@ -225,7 +227,7 @@ def test_record_then_backward_equals_combined(dev, case):
 FUSED_ADJ_CASES = [
     # (B, P, psf, lam, rho, K)
     (2, 1, None, 0.0041, 0.021, 1),
-    (1, 2, None, 0.05, 0.02, 2),
+    (1, 2, None, 0.002, 0.02, 2),      # prox live in 1.4 % of z_1
     (3, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 3),
     (2, 1, ("gauss", 9, 1.5), 0.01, 0.05, 12),
     (1, 3, None, 0.0041, 0.021, 50),   # c5 layer shape: RGB, no PSF, K=50
@@ -243,6 +245,7 @@ def test_backward_fused_adjoint(dev, case):
     h = psf(spec, rng)
     y = synth.make_batch(B, 256, 256, h, P=P, g0=21)
     xbar = rng.standard_normal(y.shape).astype(np.float32)
+    assert_case_prox_active(y, lam, rho, h, False, K, "fused adjoint " + str(case))
     ht = None if h is None else torch.from_numpy(h).to(dev)
     yt, xt = torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev)
     x, rec = admm_deconv.tvd_fft_record(yt, lam, rho, ht, False, K, need_h=False)
@@ -296,6 +299,7 @@ def test_backward_generic_shape_vs_autograd(dev, case):
     h = psf(spec, rng)
     y = synth.make_batch(B, M, N, h, P=P, g0=13)
     xbar = rng.standard_normal(y.shape).astype(np.float32)
+    assert_case_prox_active(y, lam, rho, h, iso, K, "generic " + str(case))
     ht = None if h is None else torch.from_numpy(h).to(dev)
     x, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev), torch.from_numpy(xbar).to(dev),
                                                      lam, rho, ht, iso, K)

@@ -145,3 +145,10 @@ def test_bench_two_ranks_gloo(dev):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 16
     assert "IPC push gather" in d["config"]["parallelism"] and d["value"] > 0
+    # the per-rank diagnostics of a multi-GPU record: what each rank saw and where its time went
+    assert [r["rank"] for r in d["ranks"]] == [0, 1]
+    for r in d["ranks"]:
+        assert r["world_seen"] == 2 and r["backend"] == "gloo" and r["gather_engine"] == "ipc"
+        assert r["ms_per_step"] > 0 and r["solve_only_ms_per_step"] > 0 and r["gather_tail_ms"] >= 0
+        assert r["device"] == 0 and r["visible_devices"] >= 1
+    assert d["solve_only"]["value"] > 0 and d["solve_only"]["ms_per_step"] > 0

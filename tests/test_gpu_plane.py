@@ -21,26 +21,29 @@ CASES = [
     (1, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 1),
     (1, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 2),
     (1, 1, ("gauss", 15, 2.5), 0.0041, 0.021, 3),
-    (1, 3, None, 0.05, 0.02, 12),                     # empty PSF denoiser (F2), RGB
+    (1, 3, None, 0.02, 0.02, 12),                     # empty PSF denoiser (F2), RGB (prox live in 1.3 %)
     (2, 1, ("rand", 10, 10), 0.01, 0.05, 7),          # even PSF
     (1, 1, ("rand", 4, 9), 0.02, 0.1, 5),             # asymmetric PSF
     (1, 1, ("box",), 0.0041, 0.021, 100),             # reference test PSF, default maxit
-    (3, 1, ("gauss", 9, 1.2), 0.5, 0.3, 6),           # large tau: most of s clipped
+    (3, 1, ("gauss", 9, 1.2), 0.1, 0.3, 6),           # large tau: 98 % of s clipped
+    (3, 1, ("gauss", 9, 1.2), 0.5, 0.3, 6),           # tau above every |s|: all clipped (linear-only)
 ]
+LINEAR_ONLY = {(3, 1, ("gauss", 9, 1.2), 0.5, 0.3, 6)}
 
 
 def fused_off():
     return _lib.option("FUSED", 0)
 
 
-@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}-{c[2][0] if c[2] else 'none'}-K{c[5]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}x{c[1]}-{c[2][0] if c[2] else 'none'}-K{c[5]}-lam{c[3]}" for c in CASES])
 def test_plane_vs_oracle_and_2pass(dev, case):
     B, P, psf, lam, rho, K = case
     rng = np.random.default_rng(B * 31 + P + K)
     h = make_psf(psf, rng)
     y = synth.make_batch(B, 256, 256, h, P=P, g0=11)
     got = run_gpu(dev, y, lam, rho, h, False, K)
-    ref = run_oracle(y, lam, rho, h, False, K)
+    ref = run_oracle(y, lam, rho, h, False, K, linear_only=K == 1 or case in LINEAR_ONLY,
+                     what="fused " + str(case))
     assert_parity(got, ref, what="fused " + str(case))
     with fused_off():
         two = run_gpu(dev, y, lam, rho, h, False, K)

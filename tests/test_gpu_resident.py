@@ -12,7 +12,7 @@ import torch
 import admm_deconv
 import oracle_np
 from admm_deconv import _lib, synth
-from parity import assert_parity
+from parity import assert_parity, oracle_solve
 
 pytestmark = pytest.mark.gpu
 
@@ -70,8 +70,7 @@ def test_resident_parity_vs_oracle_and_2pass(dev, case):
     assert _resident_ran(dev, y, h, K), "the resident kernel did not run for this shape"
     got = _solve(dev, y, lam, rho, h, K, True)
     two = _solve(dev, y, lam, rho, h, K, False)
-    ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), np.float32(lam),
-                                                    np.float32(rho), oracle_np.psf_from_c(h), False, K))
+    ref = oracle_solve(y, lam, rho, h, False, K, "spectral", linear_only=K == 1, what="resident " + str(case))
     assert_parity(got, ref, what="resident " + str(case))
     d = np.linalg.norm((got - two).ravel()) / np.linalg.norm(two.ravel())
     assert d < 1e-5, f"resident vs 2-pass rel-L2 {d:.2e}"

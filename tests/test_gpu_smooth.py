@@ -13,7 +13,7 @@ import admm_deconv
 import oracle_np
 import oracle_torch
 from admm_deconv import _lib, synth
-from parity import assert_parity
+from parity import assert_parity, oracle_solve
 
 pytestmark = pytest.mark.gpu
 
@@ -30,6 +30,14 @@ CASES = [
     (3, 1, 250, 250, ("gauss", 9, 1.5), 0.0041, 0.021, 6, True),     # isotropic: compiled column / line inverse
     (1, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 1, False),   # K = 1: no line update
 ]
+
+
+@pytest.fixture(autouse=True)
+def _two_pass_kernels(dev):
+    """This file covers admm_smooth.hip's 2-pass kernels: the CU-resident solve (admm_resident.hip, default at
+    the smooth squares <= 256 such as 250 x 250) is switched off here; tests/test_gpu_resident.py covers it."""
+    with _lib.option("RESIDENT", 0):
+        yield
 
 
 def _psf(spec, rng):
@@ -57,8 +65,7 @@ def test_smooth_parity_vs_oracle_and_runtime_plans(dev, case):
     got = _solve(dev, y, lam, rho, h, iso, K)
     with _lib.option("SMOOTH", 0):
         rt = _solve(dev, y, lam, rho, h, iso, K)
-    ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), np.float32(lam),
-                                                    np.float32(rho), oracle_np.psf_from_c(h), iso, K))
+    ref = oracle_solve(y, lam, rho, h, iso, K, "spectral", linear_only=K == 1, what="smooth " + str(case))
     assert_parity(got, ref, what="smooth " + str(case))
     assert_parity(rt, ref, what="runtime plans " + str(case))
     d = np.linalg.norm((got - rt).ravel()) / np.linalg.norm(rt.ravel())

@@ -10,6 +10,7 @@ import pytest
 
 import oracle_c
 import oracle_np as o
+from parity import PROX_MIN_FRACTION
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -102,14 +103,41 @@ def test_st_and_pixelnorm():
     assert np.allclose(o.pixelnorm(v), np.sqrt(8.0))   # over ALL channels and P (dims 3,4)
 
 
+def test_prox_stats_separate_linear_from_live_cases():
+    """oracle_np's prox statistics (tests/parity.py assert_prox_active): K = 1 records nothing (the K-th z is
+    dead); the reference demo shape (32 x 32 PSF on 32 x 32 crops, src/ADMM_Deconv.jl:17-23) at tau = 0.05 / 0.3
+    never fires (every |Dx| is below tau), at tau = 0.0005 / 0.3 it does; the two forms agree."""
+    from admm_deconv import synth
+    rng = np.random.default_rng(2 * 1000 + 32 + 32 + 50)
+    h = rng.random((32, 32)).astype(np.float32)
+    h = (h / h.sum()).astype(np.float32)
+    y = synth.make_batch(2, 32, 32, h, P=3, g0=7).astype(np.float64)
+    fr = {}
+    for lam in (0.05, 0.0005):
+        for f in (o.tvd_fft_literal, o.tvd_fft_spectral):
+            st = {}
+            f(o.from_c(y), np.float32(lam), np.float32(0.3), o.psf_from_c(h), False, 50, stats=st)
+            assert len(st["prox_active"]) == 49
+            fr[lam, f.__name__] = o.prox_active_fraction(st)
+    assert fr[0.05, "tvd_fft_literal"] == 0.0 == fr[0.05, "tvd_fft_spectral"]
+    assert fr[0.0005, "tvd_fft_literal"] >= PROX_MIN_FRACTION
+    assert abs(fr[0.0005, "tvd_fft_literal"] - fr[0.0005, "tvd_fft_spectral"]) < 1e-3
+    st = {}
+    o.tvd_fft_literal(o.from_c(y), np.float32(0.0005), np.float32(0.3), o.psf_from_c(h), False, 1, stats=st)
+    assert o.prox_active_fraction(st) == 0.0
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "*.npz"))), ids=os.path.basename)
 def test_golden_fixture_reproduces(path):
     d = np.load(path)   # allow_pickle=False (default)
     p = json.loads(str(d["params"]))
     h = d["h"] if d["h"].size else None
+    st = {}
     x = o.to_c(o.tvd_fft_literal(o.from_c(d["y"].astype(np.float64)), np.float32(p["lam"]), np.float32(p["rho"]),
-                                 o.psf_from_c(h), p["iso"], p["K"]))
+                                 o.psf_from_c(h), p["iso"], p["K"], stats=st))
     assert np.abs(x - d["x"]).max() <= 1e-6 * max(1.0, np.abs(x).max())
+    # every fixture pins the nonlinear solve: its prox fired
+    assert o.prox_active_fraction(st) >= PROX_MIN_FRACTION, (path, o.prox_active_fraction(st))
     if p["M"] * p["N"] <= 64 * 128:
         c = oracle_c.tvd_fft_c(d["y"], p["lam"], p["rho"], h, p["iso"], p["K"], np.float64, nthreads=2)
         assert np.abs(c - d["x"]).max() <= 1e-6 * max(1.0, np.abs(c).max())
