@@ -9,10 +9,13 @@
 // s = Dx + u (read + write, 8 B/px each) and H^T y (4 B/px): 20 B/px, as in the 256^2 kernel
 // (plane_kernel.hip).
 //
-// Register layout: thread t = k * LS + jt (LS = 512 / H line slots) holds bin k of lines jt, jt + LS, ...:
-// S[r] = X(line r LS + jt, bin k).  So a bin's column lives in LS threads at consecutive registers and a
-// line chunk is a fixed register range: both staging directions are plain LDS stores at compile-time
-// offsets, no index arithmetic per element.
+// Register layout: the H bins are dealt into NCC column chunks of KBC bins; thread t = kk * LS + jt (LS = 512 /
+// KBC line slots) holds bin c KBC + kk of every chunk c, lines jt, jt + LS, ...:
+// S[c NR + r] = X(line r LS + jt, bin c KBC + kk).  A column chunk is register range c and a line chunk
+// (a multiple of LS lines) register range r, so every thread takes part in every phase and no register is
+// ever written under a lane condition: a lane-conditional write keeps the old value live next to the new
+// one (a phi the register allocator resolves with copies), which at 250^2 cost 288 B/lane of spills.
+// Both staging directions are plain LDS accesses at compile-time offsets from a per-thread base.
 //
 // Per iteration:
 //   column phase  per chunk of KBC bins: S -> LDS [bin][line], dim-2 FFT (compile-time Stockham plan,
@@ -44,6 +47,12 @@ constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 p
 #endif
 #ifndef RS_RAD
 #define RS_RAD 16
+#endif
+#ifndef RS_PINSEP
+#define RS_PINSEP 1
+#endif
+#ifndef RS_U2MAX
+#define RS_U2MAX 10
 #endif
 constexpr int kRad = RS_RAD;              // radix cap of every transform
 constexpr int kLdsBytes = 160 * 1024;     // gfx950 LDS per CU
@@ -190,7 +199,10 @@ __device__ __forceinline__ void ipass(int cnt, const float2* __restrict__ tw, Ac
         }
     };
     // two butterflies in flight for small radices; one for R > 10 (register pressure next to the spectrum)
-    constexpr int U = R <= 10 ? 2 : 1;
+    constexpr int U = R <= RS_U2MAX ? 2 : 1;
+    // not unrolled: with a compile-time trip count the compiler would interleave the butterflies of several
+    // iterations (2 U in flight: ~136 VGPRs of butterfly values next to the spectrum, the 250^2 spills)
+#pragma unroll 1
     for (int i0 = tid(); i0 < total; i0 += U * kNT) {
         const int i1 = i0 + kNT;
         int f0, b0, j0, f1 = 0, b1 = 0, j1 = 0;
@@ -234,30 +246,42 @@ __device__ __forceinline__ void dit_passes(int cnt, const float2* tw, Acc<FS> a)
 template <int MM, int NN>
 struct Geo {
     static constexpr int H = MM / 2 + 1;           // bins per line
-    static constexpr int LS = (kNT / H) & ~1;      // line slots (even: lines 2f, 2f + 1 in neighbouring lanes)
-    static constexpr int NR = cdiv(NN, LS);        // spectrum registers per thread
-    static constexpr int FS = NN | 1;              // column stride (odd: neighbouring columns on distinct banks)
-    static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
     static constexpr int kBudget = (kLdsBytes - 512) / 8 - MM - NN;   // float2 slots for the main buffer
-    static constexpr int ncc() {
-        for (int n = 1; n <= H; ++n)
-            if (cdiv(H, n) * FS <= kBudget) return n;
-        return 0;
+    // column chunks n: KBC bins each, LS line slots (even: lines 2f, 2f + 1 in neighbouring lanes), NR
+    // registers per chunk; the column buffer holds KBC columns of stride FS >= NR LS (odd: neighbouring
+    // columns on distinct banks), so the read-back of a register's padding lines stays in its own column
+    static constexpr int kbc(int n) { return cdiv(H, n); }
+    static constexpr int ls(int n) { return (kNT / kbc(n)) & ~1; }
+    static constexpr int nr(int n) { return cdiv(NN, ls(n)); }
+    static constexpr int fs(int n) { return (nr(n) * ls(n)) | 1; }
+    static constexpr bool fits(int n) { return ls(n) >= 2 && kbc(n) * fs(n) <= kBudget; }
+    static constexpr int ncc() {   // fewest spectrum registers, then fewest chunks
+        int best = 0;
+        for (int n = 1; n <= 8 && n <= H; ++n)
+            if (fits(n) && (best == 0 || n * nr(n) < best * nr(best))) best = n;
+        return best;
     }
-    static constexpr int tl(int n) { return (cdiv(NN, n) + 1) & ~1; }
-    static constexpr int nlc() {   // line chunks: T lines + a halo pair either side, as complex line pairs
+    static constexpr int NCC = ncc();              // column chunks
+    static constexpr int KBC = kbc(NCC);           // bins per column chunk
+    static constexpr int LS = ls(NCC);             // line slots
+    static constexpr int NR = nr(NCC);             // registers per column chunk
+    static constexpr int NREG = NCC * NR;          // spectrum registers (float2) per thread
+    static constexpr int FS = fs(NCC);
+    static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
+    // line chunks: TL lines (a multiple of LS: whole registers) + a halo pair either side, as complex pairs
+    static constexpr int tl(int n) { return cdiv(cdiv(NN, n), LS) * LS; }
+    static constexpr int nlc() {
         for (int n = 1; n <= NN; ++n)
             if ((tl(n) / 2 + 2) * MM <= kBudget) return n;
         return 0;
     }
-    static constexpr int NCC = ncc();              // column chunks
-    static constexpr int KBC = cdiv(H, NCC);       // bins per column chunk
     static constexpr int NLC = nlc();              // line chunks
-    static constexpr int TL = tl(NLC);             // lines per line chunk (even)
+    static constexpr int TL = tl(NLC);             // lines per line chunk
     static constexpr int BUF = imax(KBC * FS, (TL / 2 + 2) * MM);
     static constexpr size_t lds_bytes() { return (size_t)(MM + NN + BUF) * 8; }
     static_assert(MM % 2 == 0 && NN % 2 == 0 && MM <= 256 && NN <= 256, "resident kernel: even M, N <= 256");
-    static_assert(LS >= 2 && NCC >= 1 && NLC >= 1, "resident kernel: shape does not fit one CU");
+    static_assert(NCC >= 1 && NLC >= 1, "resident kernel: shape does not fit one CU");
+    static_assert(LS % 2 == 0 && TL % 2 == 0, "line pairs within a lane pair");
     static_assert(Rad<MM>::P >= 2 && Rad<NN>::P >= 2, "plans of >= 2 passes");
 };
 
@@ -265,32 +289,31 @@ struct Thr {
     float2* buf;          // main LDS buffer
     const float2* twm;    // LDS twiddles exp(-2 pi i n / M), exp(-2 pi i n / N)
     const float2* twn;
-    int k, jt;            // bin, line slot
-    bool act;             // t < H LS
+    int kk, jt;           // bin within a column chunk, line slot
+    bool act;             // kk < KBC
 };
 template <int MM, int NN>
 __device__ __forceinline__ Thr thr_of(float2* buf, const float2* twm, const float2* twn) {
-    constexpr int H = MM / 2 + 1, LS = (kNT / H) & ~1;
+    using G = Geo<MM, NN>;
     const unsigned t = (unsigned)tid();
-    return {buf, twm, twn, (int)(t / LS), (int)(t % LS), t < (unsigned)(H * LS)};
+    return {buf, twm, twn, (int)(t / G::LS), (int)(t % G::LS), t < (unsigned)(G::KBC * G::LS)};
 }
 
-// ---- column phase, chunk C: bins [kc0, kc1) --------------------------------------------------------------
-template <int MM, int NN, int C, int NR>
-__device__ __forceinline__ void column_chunk(float2 (&S)[NR], const Thr& th0, const float* __restrict__ Ct) {
+// ---- column phase, chunk C: bins [kc0, kc1) = registers [C NR, C NR + NR) ---------------------------------
+template <int MM, int NN, int C, int NREG>
+__device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
     using G = Geo<MM, NN>;
     const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
     using RD = Rad<NN>;
     constexpr int kc0 = C * G::KBC, kc1 = imin(G::H, kc0 + G::KBC), kc = kc1 - kc0;
-    constexpr int KB = G::KBC, FS = G::FS, H = G::H, P = RD::P;
+    constexpr int KB = G::KBC, FS = G::FS, H = G::H, P = RD::P, NR = G::NR, R0 = C * NR;
     float2* buf = th.buf;
-    const bool mine = th.act && th.k >= kc0 && th.k < kc1;
-    if (mine) {
-        float2* col = buf + (th.k - kc0) * FS;
+    if (th.kk < kc) {   // stores only: the spectrum registers are not written here
+        float2* col = buf + th.kk * FS;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int j = r * G::LS + th.jt;
-            if (r < NR - 1 || j < NN) col[j] = S[r];
+            if (r < NR - 1 || j < NN) col[j] = S[R0 + r];
         }
     }
     __syncthreads();
@@ -300,17 +323,20 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NR], const Thr& th0, co
     {
         constexpr int R = RD::r(P - 1), Q = NN / R, WL = RD::W(P - 1);
         constexpr int NB = cdiv(KB * Q, kNT);
-        // every multiplier load of the thread's butterflies first: one L2 latency per chunk, not one per butterfly
+        // every multiplier load of the thread's butterflies first: one L2 latency per chunk, not one per butterfly.
+        // Buffer loads: one VGPR offset per butterfly, the multiplier's row m W_L H as a constant SGPR offset
+        // (global loads would hold a 64-bit address per multiplier: 2 R NB VGPRs next to the spectrum)
         const int t0 = tid();
+        const rsrc_t rc = make_rsrc(Ct, (unsigned)(H * NN * 4));
         float cm[NB][R];
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             const int idx = t0 + u * kNT;
             if (u < NB - 1 || idx < KB * Q) {
                 const int b = idx / KB, f = idx - b * KB;
-                const float* cp = Ct + (size_t)dlast<NN>(b) * H + kc0 + (f < kc ? f : 0);
+                const unsigned vo = 4u * (unsigned)(dlast<NN>(b) * H + kc0 + (f < kc ? f : 0));
 #pragma unroll
-                for (int m = 0; m < R; ++m) cm[u][m] = cp[(size_t)m * WL * H];
+                for (int m = 0; m < R; ++m) cm[u][m] = bld1(rc, vo, 4u * (unsigned)(m * WL * H));
             }
         }
 #pragma unroll
@@ -332,13 +358,11 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NR], const Thr& th0, co
     }
     __syncthreads();
     dit_passes<NN, 0, P - 1, true, false, FS>(KB, th.twn, a);
-    if (mine) {
-        const float2* col = buf + (th.k - kc0) * FS;
+    {   // every thread reads back every register of the chunk (threads past the chunk's bins: a valid column,
+        // values never used; padding lines j >= NN: the column's padding slots, never used either)
+        const float2* col = buf + imin(th.kk, kc - 1) * FS;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int j = r * G::LS + th.jt;
-            if (r < NR - 1 || j < NN) S[r] = col[j];
-        }
+        for (int r = 0; r < NR; ++r) S[R0 + r] = col[r * G::LS + th.jt];
     }
     __syncthreads();
 }
@@ -392,44 +416,48 @@ __device__ __forceinline__ float2 zsep(float2 z, float2 zm, bool odd) {
     return make_float2(0.5f * (px + qx), 0.5f * (py + qy));
 }
 
-// hs[c]: chunk c's halo-A register (lines jc0 - 2, jc0 - 1) for c >= 1, hs[0] the register of lines 0, 1 (the
-// last chunk's halo B), saved before the update phase: by the time a chunk stages them, the chunk that owns
-// those lines has already replaced them with the next iteration's spectra.
-template <int MM, int NN, int C, int MODE, int NR, int NH>
-__device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[NH], const Thr& th0, const LineArgs& a) {
+// hs[C NCC + c]: for C >= 1 chunk C's halo-A register (lines jc0 - 2, jc0 - 1) of column chunk c, for C = 0 the
+// register of lines 0, 1 (the last chunk's halo B), saved before the update phase: by the time a chunk stages
+// them, the chunk that owns those lines has already replaced them with the next iteration's spectra.
+template <int MM, int NN, int C, int MODE, int NREG, int NH>
+__device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)[NH], const Thr& th0, const LineArgs& a) {
     using G = Geo<MM, NN>;
     const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
     using RD = Rad<MM>;
-    constexpr int LS = G::LS, P = RD::P;
+    constexpr int LS = G::LS, P = RD::P, NR = G::NR, NCC = G::NCC, KBC = G::KBC, H = G::H;
     constexpr int jc0 = C * G::TL, jc1 = imin(NN, jc0 + G::TL), T = jc1 - jc0;
+    constexpr int rc0 = jc0 / LS, rc1 = cdiv(jc1, LS);   // the chunk's registers (the last may hold lines >= NN)
     constexpr int HP = MODE == kUpdate ? 1 : 0;   // halo pairs either side
     constexpr int NP = T / 2 + 2 * HP;            // pairs staged
     float2* buf = th.buf;
     float* Xf = reinterpret_cast<float*>(buf);
     const Acc<MM> al{buf};
+    const bool odd = th.jt & 1;
 
     if constexpr (MODE != kInit) {
-        // ---- S -> z pairs, inverse DIF (x at dpos order) ----
-        if (th.act) {
-            const ZLane zl = zlane<MM>(th.k, th.jt & 1);
-            float2* zb = buf + (th.jt >> 1) * MM + zl.slot;   // + pair offset of register r
+        // ---- S -> z pairs (stores only), inverse DIF (x at dpos order) ----
+        float2* zb0 = buf + (th.jt >> 1) * MM;   // + z slot + pair offset of register r
+        static_for<0, NCC>([&](auto ic) {
+            constexpr int c = decltype(ic)::value;
+            const int k = c * KBC + th.kk;
+            const bool kv = th.act && k < H;      // lanes past the last chunk's bins store nothing
+            const ZLane zl = zlane<MM>(k, odd);
+            float2* zb = zb0 + zl.slot;
 #pragma unroll
-            for (int r = jc0 / LS; r <= (jc1 - 1) / LS; ++r) {
-                const int j = r * LS + th.jt;
-                const float2 z = zval(S[r], lane_swap(S[r]), zl);
-                if ((r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1))
-                    zb[((r * LS - jc0) / 2 + HP) * MM] = z;
+            for (int r = rc0; r < rc1; ++r) {
+                const float2 z = zval(S[c * NR + r], lane_swap(S[c * NR + r]), zl);
+                if (kv && (r < rc1 - 1 || r * LS + th.jt < jc1)) zb[((r * LS - jc0) / 2 + HP) * MM] = z;
             }
             if constexpr (HP) {
                 constexpr int hA = (jc0 + NN - 2) % NN, hB = jc1 % NN;   // even lines: pairs (hA, hA+1), (hB, hB+1)
-                const float2 sA = C >= 1 ? hs[C] : S[hA / LS];
+                const float2 sA = C >= 1 ? hs[C * NCC + c] : S[c * NR + hA / LS];
                 const float2 zA = zval(sA, lane_swap(sA), zl);
-                if ((th.jt >> 1) == (hA % LS) / 2) buf[zl.slot] = zA;
-                const float2 sB = (C == G::NLC - 1 && G::NLC > 1) ? hs[0] : S[hB / LS];
+                if (kv && (th.jt >> 1) == (hA % LS) / 2) buf[zl.slot] = zA;
+                const float2 sB = (C == G::NLC - 1 && G::NLC > 1) ? hs[c] : S[c * NR + hB / LS];
                 const float2 zB = zval(sB, lane_swap(sB), zl);
-                if ((th.jt >> 1) == (hB % LS) / 2) buf[(NP - 1) * MM + zl.slot] = zB;
+                if (kv && (th.jt >> 1) == (hB % LS) / 2) buf[(NP - 1) * MM + zl.slot] = zB;
             }
-        }
+        });
         __syncthreads();
         dif_passes<MM, 0, P, true, true, MM>(NP, th.twm, al);
     }
@@ -595,20 +623,24 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NR], const float2 (&hs)[N
         dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, al);
     }
     // ---- half spectra separated into S: X_2f = (z + conj z(-k)) / 2, X_2f+1 = (z - conj z(-k)) / (2i) ----
-    // (Only the threads that hold spectrum bins.  Reading into every thread's registers unconditionally, so
-    // that the chunk's old registers die early, measured 68k vs 78k img/s at 250^2: more scratch, not less.)
-    if (th.act) {
-        const int k = th.k, km = k == 0 ? 0 : MM - k;
-        const bool odd = th.jt & 1;
+    // Every thread, every register of the chunk: lanes past the last column chunk's bins take bin H - 1 and
+    // padding lines (j >= NN) read pairs inside the buffer; neither value is ever used.
+    {
         const float2* Zb = buf + ((th.jt >> 1) + HP) * MM;   // + pair offset of register r
+        static_for<0, NCC>([&](auto ic) {
+            constexpr int c = decltype(ic)::value;
+            const int k = imin(c * KBC + th.kk, H - 1), km = k == 0 ? 0 : MM - k;
 #pragma unroll
-        for (int r = jc0 / LS; r <= (jc1 - 1) / LS; ++r) {
-            const int j = r * LS + th.jt;
-            if ((r * LS >= jc0 || j >= jc0) && ((r + 1) * LS <= jc1 || j < jc1)) {
+            for (int r = rc0; r < rc1; ++r) {
                 const float2* Z = Zb + ((r * LS - jc0) / 2) * MM;
-                S[r] = zsep(Z[k], Z[km], odd);
+                S[c * NR + r] = zsep(Z[k], Z[km], odd);
+#if RS_PINSEP
+                // formed here: left free, the compiler sinks zsep to the next use (the next iteration) and keeps
+                // both loaded halves live instead, twice the registers
+                __asm__ volatile("" : "+v"(S[c * NR + r].x), "+v"(S[c * NR + r].y));
+#endif
             }
-        }
+        });
     }
     __syncthreads();
 }
@@ -628,7 +660,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g * (unsigned)stagger) __builtin_amdgcn_s_sleep(10);
     }
-    constexpr int NR = G::NR;
+    constexpr int NREG = G::NREG, NR = G::NR, NCC = G::NCC;
     constexpr size_t MN = (size_t)MM * NN;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* twm = reinterpret_cast<float2*>(smem_raw);
@@ -641,9 +673,9 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     th.buf = twn + NN;
     th.twm = twm;
     th.twn = twn;
-    th.k = (int)(t / G::LS);
+    th.kk = (int)(t / G::LS);
     th.jt = (int)(t % G::LS);
-    th.act = t < (unsigned)(G::H * G::LS);
+    th.act = t < (unsigned)(G::KBC * G::LS);
     LineArgs la;
     la.hty = hty_all + plane * MN;
     la.xo = x_all + plane * MN;
@@ -652,11 +684,11 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     la.so = nullptr;
     la.sn = nullptr;
     la.first = true;
-    float2 S[NR];
+    float2 S[NREG];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) S[r] = make_float2(0.f, 0.f);
+    for (int r = 0; r < NREG; ++r) S[r] = make_float2(0.f, 0.f);
     __syncthreads();
-    float2 hs[G::NLC];
+    float2 hs[G::NLC * NCC];
     static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kInit>(S, hs, th, la); });
 #pragma unroll 1
     for (int it = 1; it <= maxit; ++it) {
@@ -679,10 +711,12 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
         la.sn = sn + plane * 2 * MN;
         la.so = so + plane * 2 * MN;
         la.first = it == 1;
-        hs[0] = S[0];
+#pragma unroll
+        for (int c = 0; c < NCC; ++c) hs[c] = S[c * NR];
         static_for<1, G::NLC>([&](auto ic) {
-            constexpr int c = decltype(ic)::value;
-            hs[c] = S[(c * G::TL - 2) / G::LS];
+            constexpr int C = decltype(ic)::value;
+#pragma unroll
+            for (int c = 0; c < NCC; ++c) hs[C * NCC + c] = S[c * NR + (C * G::TL - 2) / G::LS];
         });
 #ifndef RS_SKIP_UPD
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kUpdate>(S, hs, th, la); });
@@ -699,8 +733,9 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #endif
 
 // Compiled shapes where the 2-pass smooth kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the
-// 2-pass path; 2 forces the resident kernel on every compiled shape)
-#define RS_SLOWER(X) X(240, 240)
+// 2-pass path; 2 forces the resident kernel on every compiled shape).  None since the spills went (round 4:
+// 240^2 resident 77.8k img/s vs 74.2k 2-pass, profiles/r04_resident_shapes.jsonl).
+#define RS_SLOWER(X)
 
 bool has_shape(int M, int N, bool all) {
 #define X(m, n) \

@@ -189,15 +189,15 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     # rho), the scale an exact summation in any precision is judged by; the relative-to-value error is logged
     lam_scale = max(sc["tau"] / R, abs(lb0))
     rho_scale = max(sc["rho"] + sc["tau"] * L / (R * R), abs(rb0))
-    _, yb32, hb32, lb32, rb32 = oracle_torch.tvd_fft_grads(y, lam32, rho32, h, iso, K, xbar, dtype=torch.float32,
-                                                           masks=masks)
+    x32, yb32, hb32, lb32, rb32 = oracle_torch.tvd_fft_grads(y, lam32, rho32, h, iso, K, xbar, dtype=torch.float32,
+                                                             masks=masks)
     err = {"x": _plane_rel(x.cpu().numpy(), x0), "y_bar": _plane_rel(yb.cpu().numpy(), yb0),
            "lambda_bar": abs(float(lb) - lb0) / max(lam_scale, 1e-300)}
     if need_rho:
         err["rho_bar"] = abs(float(rb) - rb0) / max(rho_scale, 1e-300)
     else:
         assert rb is None
-    ref32 = {"y_bar": _plane_rel(yb32, yb0), "lambda_bar": abs(lb32 - lb0) / max(lam_scale, 1e-300),
+    ref32 = {"x": _plane_rel(x32, x0), "y_bar": _plane_rel(yb32, yb0), "lambda_bar": abs(lb32 - lb0) / max(lam_scale, 1e-300),
              "rho_bar": abs(rb32 - rb0) / max(rho_scale, 1e-300)}
     if hb is not None:
         err["h_bar"] = _rel(hb.cpu().numpy(), hb0)
