@@ -38,7 +38,8 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
-           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async")
+           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths",
+           "admm_path_name")
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
 REC_HBAR, REC_MASKS = 1, 2
@@ -148,6 +149,10 @@ def load():
     L.admm_profile_get.argtypes = [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
     L.admm_copy_async.restype = c_int
     L.admm_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
+    L.admm_query_paths.restype = c_int
+    L.admm_query_paths.argtypes = [c_int] * 8 + [ctypes.POINTER(c_int)] * 2
+    L.admm_path_name.restype = ctypes.c_char_p
+    L.admm_path_name.argtypes = [c_int]
     _lib = L
     return L
 
@@ -177,6 +182,18 @@ def multi_workspace_bytes(M, N, P, B, nbranch, maxit, flags):
     out = ctypes.c_size_t(0)
     check(load().admm_tvd_multi_workspace_bytes(M, N, P, B, nbranch, int(maxit), int(flags), ctypes.byref(out)))
     return out.value
+
+
+MODE_FORWARD, MODE_RECORD, MODE_BACKWARD = 0, 1, 2
+
+
+def query_paths(M, N, iso=False, kh=0, mode=MODE_FORWARD, flags=0, want_hbar=False, want_rho=False):
+    """admm_query_paths: (forward path name, reverse-sweep path name or None) the library would run."""
+    L = load()
+    f, b = ctypes.c_int(0), ctypes.c_int(0)
+    check(L.admm_query_paths(M, N, int(iso), kh, mode, flags, int(want_hbar), int(want_rho), ctypes.byref(f),
+                             ctypes.byref(b)))
+    return L.admm_path_name(f.value).decode(), (L.admm_path_name(b.value).decode() if b.value else None)
 
 
 def copy_async(dst, src, nbytes, stream):

@@ -206,12 +206,17 @@ def chcat(*xs):
     return torch.cat(xs, dim=1)
 
 
+# isotropic branches are merged into one grid by default when all their planes fit one wave of workgroups
+ISO_MERGE_MAX_PLANES = 256
+
+
 class Parallel:
     """Flux `Parallel(connection, layers...)` as the nets build it (net_build.jl:121-125, :175): every
     branch sees the same input and `connection` combines the branch outputs.
 
     When every branch is an ADMM layer the one-grid solve covers (the denoiser: ADMMDeconvF2((), K, ρ_i, σ),
-    256 x 256, same K and prox; isotropic only with merge="always" and no ρ needing a gradient), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
+    256 x 256, same K and prox; isotropic when no ρ needs a gradient and the branches' planes fit one wave of
+    workgroups, ISO_MERGE_MAX_PLANES, or with merge="always"), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
     planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
     each branch's bias and σ then apply to its slice.  The forward output, λ̄ and ρ̄ are bitwise those of the
     branches run one by one; the input gradient matches them to fp32 rounding (branch_sum_kernel adds the
@@ -234,12 +239,18 @@ class Parallel:
         if not all(isinstance(L, Admm) for L in Ls):
             return False
         K, iso = Ls[0].iters, Ls[0].iso
-        # isotropic: only on request (merge="always").  Its one-grid solve is a launch per iteration either way,
-        # and the branches on their own streams overlap one branch's batch-norm launches with the others'
-        # plane launches: c5 iso 1.10k img/s per-branch against 0.97k in one grid (profiles/r03_c5iso_*.json).
-        # It forms no rho_bar either.
-        if iso and (self.merge != "always" or any(self._needs_rho(L) for L in Ls)):
-            return False
+        # isotropic: its one-grid solve is a launch per iteration either way.  When every branch's planes together
+        # fit one wave of workgroups (<= ISO_MERGE_MAX_PLANES, one plane per CU), one grid per iteration halves the
+        # launches and the chip is not full anyway: the reference's training batch (train_cfg.json batch_size 2,
+        # 5 branches x 6 planes) runs 229 img/s merged against 119 per-branch.  Above that, the branches on their
+        # own streams overlap one branch's batch-norm launches with the others' plane launches: batch 64 (960
+        # planes) 1.11k img/s per-branch against 1.03k merged (profiles/r04_c5_configs.jsonl).  merge="always"
+        # merges at any size.  The merged grid forms no rho_bar.
+        if iso:
+            if any(self._needs_rho(L) for L in Ls):
+                return False
+            if self.merge != "always" and len(Ls) * x.shape[0] * x.shape[1] > ISO_MERGE_MAX_PLANES:
+                return False
         return all(L.iters == K and L.iso == iso and L.weight.numel() == 0 and L.group is None for L in Ls) and \
             multi_supported(x, iso)
 

@@ -355,6 +355,95 @@ struct Traj {
     bool iso_lane = false;   // isotropic 256 x 256: s and nrm lane-native (plane_iso.hip), for the fused adjoint
 };
 
+// ---- path selection: ONE decision table for every entry point -----------------------------------------------
+// Which kernels a call runs is decided here and nowhere else; run_forward / run_forward_generic / run_backward
+// only execute the plan, and admm_query_paths (include/admm_deconv.h) returns it to tests without a GPU.
+// Inputs: shape, prox, PSF, what the call is (plain forward, recording with ADMM_REC_* flags, combined
+// backward with or without h_bar / rho_bar) and the library options.
+struct PathIn {
+    int M, N;
+    bool iso, psf;
+    int mode;            // ADMM_MODE_FORWARD, ADMM_MODE_RECORD, ADMM_MODE_BACKWARD
+    int rec_flags;       // ADMM_REC_* (record)
+    bool h_bar, rho_bar; // backward: gradients asked for
+};
+struct PathPlan {
+    bool want_h = false;     // the forward records the dim-2 spectra h_bar needs (2-pass column pass)
+    bool ln_traj = false;    // the fused 256^2 forward records s lane-native
+    bool masks = false;      // ADMM_REC_MASKS honoured: ST mask bits (aniso) / lane-native s and |s| (iso)
+    bool iso_lane = false;   // the fused isotropic trajectory + sweep
+    int fwd = 0;             // ADMM_PATH_* of the forward
+    int bwd = 0;             // ADMM_PATH_SWEEP_* of the reverse sweep (0: none)
+};
+// the trajectory a recording keeps, as run_forward sees it (pointers only matter as null / non-null)
+struct TrajFlags {
+    bool s, v, nrm, m, iso_lane;
+};
+TrajFlags traj_flags(const PathIn& q, const PathPlan& pl) {
+    if (q.mode == ADMM_MODE_FORWARD) return {false, false, false, false, false};
+    return {true, pl.want_h, q.iso, pl.masks && !q.iso, pl.iso_lane};
+}
+// forward rules, first match wins
+struct FwdRule {
+    int path;
+    bool (*applies)(const PathIn&, const TrajFlags&);
+};
+const FwdRule kFwdRules[] = {
+    // runtime-length shapes: the CU-resident solve (admm_resident.hip) where compiled and measured faster,
+    // anisotropic and recording neither dim-2 spectra, norms nor mask bits (it writes s_k into the slots)
+    {ADMM_PATH_RESIDENT, [](const PathIn& q, const TrajFlags& t) {
+         return generic_shape(q.M, q.N) && !q.iso && !t.v && !t.nrm && !t.m && opt(ADMM_OPT_RESIDENT) != 0 &&
+                opt(ADMM_OPT_SMOOTH) != 0 && admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
+     }},
+    // compile-time-plan kernels when this build has either length (admm_smooth.hip), else runtime plans
+    {ADMM_PATH_SMOOTH, [](const PathIn& q, const TrajFlags&) {
+         return generic_shape(q.M, q.N) && opt(ADMM_OPT_SMOOTH) != 0 &&
+                (admm::sm::has_length(q.M) || admm::sm::has_length(q.N));
+     }},
+    {ADMM_PATH_RUNTIME, [](const PathIn& q, const TrajFlags&) { return generic_shape(q.M, q.N); }},
+    // 256 x 256 anisotropic: one workgroup per plane runs all K iterations (plane_kernel.hip)
+    {ADMM_PATH_FUSED, [](const PathIn& q, const TrajFlags& t) {
+         return fused_shape(q.M, q.N, q.iso) && !t.v && fused_enabled();
+     }},
+    // 256 x 256 isotropic: split-iteration per-plane kernels (plane_iso.hip); a recording only in its own
+    // lane-native layout (the fused sweep's)
+    {ADMM_PATH_FUSED_ISO, [](const PathIn& q, const TrajFlags& t) {
+         return q.iso && fused_tables_shape(q.M, q.N) && (!t.s || t.iso_lane) && !t.v && fused_enabled();
+     }},
+    {ADMM_PATH_2PASS_ISO, [](const PathIn& q, const TrajFlags&) { return q.iso; }},
+    {ADMM_PATH_2PASS, [](const PathIn&, const TrajFlags&) { return true; }},
+};
+
+PathPlan plan_paths(const PathIn& q) {
+    PathPlan pl;
+    const bool rec = q.mode != ADMM_MODE_FORWARD;
+    if (rec) {
+        pl.want_h = (q.mode == ADMM_MODE_RECORD ? (q.rec_flags & ADMM_REC_HBAR) != 0 : q.h_bar) && q.psf;
+        // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
+        pl.ln_traj = fused_shape(q.M, q.N, q.iso) && fused_enabled() && !pl.want_h;
+        // mask-bit trajectory (fused forward + fused reverse sweep): asked for by a recording (ADMM_REC_MASKS),
+        // taken by the combined call whenever rho_bar is not wanted; isotropic at 256 x 256 the same flag
+        // selects the split-iteration trajectory (s and |s| lane-native) for the fused isotropic sweep
+        const bool iso_ok = q.iso && fused_tables_shape(q.M, q.N) && !pl.want_h && fused_enabled() && fused_adj_enabled();
+        const bool masks_ok = (pl.ln_traj && !q.iso && fused_adj_enabled()) || iso_ok;
+        pl.masks = masks_ok && (q.mode == ADMM_MODE_RECORD ? (q.rec_flags & ADMM_REC_MASKS) != 0 : !q.rho_bar);
+        pl.iso_lane = pl.masks && q.iso;
+    }
+    const TrajFlags t = traj_flags(q, pl);
+    for (const FwdRule& r : kFwdRules)
+        if (r.applies(q, t)) {
+            pl.fwd = r.path;
+            break;
+        }
+    if (rec) {
+        if (pl.ln_traj && !q.iso && fused_adj_enabled()) pl.bwd = ADMM_PATH_SWEEP_FUSED;         // plane256_adj_kernel
+        else if (pl.iso_lane) pl.bwd = ADMM_PATH_SWEEP_FUSED_ISO;                                   // plane256_isoadj
+        else if (generic_shape(q.M, q.N)) pl.bwd = q.iso ? ADMM_PATH_SWEEP_RUNTIME_ISO : ADMM_PATH_SWEEP_RUNTIME;
+        else pl.bwd = q.iso ? ADMM_PATH_SWEEP_2PASS_ISO : ADMM_PATH_SWEEP_2PASS;
+    }
+    return pl;
+}
+
 // Shared forward: everything admm_tvd_forward_f32 does, plus optional trajectory recording.
 // Returns the Launcher's status; `ln` keeps the events for the profiler.
 // ---- generic-size path (admm_generic.hip) ----------------------------------------------------
@@ -407,7 +496,7 @@ size_t gen_lds_col(int N, int KB) { return (size_t)2 * KB * N * 8 + (size_t)N * 
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
                         int iso, int maxit, unsigned char* ws, const Layout& lay,
-                        const Traj& tr, const admm_batch_reducer* red);
+                        const Traj& tr, const admm_batch_reducer* red, int path);
 
 // the caller's cross-shard sum of an M x N map (isotropic prox over a sharded batch)
 int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStream_t s) {
@@ -418,7 +507,7 @@ int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStr
 
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
                 int kw, const admm::ScalarSrc& sc, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                const Traj& tr, const admm_batch_reducer* red) {
+                const Traj& tr, const admm_batch_reducer* red, int fwd_path) {
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
     const size_t MN = (size_t)M * N;
@@ -449,10 +538,11 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         return ADMM_OK;
     }
 
-    if (generic_shape(M, N)) {
-        return run_forward_generic(ln, y, x_out, M, N, planes, kh, iso, maxit, ws, lay, tr, red);
+    const int path = fwd_path;
+    if (path == ADMM_PATH_RESIDENT || path == ADMM_PATH_SMOOTH || path == ADMM_PATH_RUNTIME) {
+        return run_forward_generic(ln, y, x_out, M, N, planes, kh, iso, maxit, ws, lay, tr, red, path);
     }
-    if (fused_shape(M, N, iso != 0) && !tr.v && fused_enabled()) {
+    if (path == ADMM_PATH_FUSED) {
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
         // spec0, lane-native s in sA -- or, recording a trajectory, s_k in its own slot of tr.s
         namespace pk = admm::plane;
@@ -466,7 +556,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         });
         return rc;
     }
-    if (iso && fused_tables_shape(M, N) && (!tr.s || tr.iso_lane) && !tr.v && fused_enabled()) {
+    if (path == ADMM_PATH_FUSED_ISO) {
         // isotropic at 256 x 256: the split-iteration per-plane kernels (plane_iso.hip), the spectrum
         // resident in the CU; per iteration one plane256_iso_kernel and one iso_norm_kernel (batch norm)
         namespace pk = admm::plane;
@@ -597,7 +687,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
 
 int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, int kh,
                         int iso, int maxit, unsigned char* ws, const Layout& lay,
-                        const Traj& tr, const admm_batch_reducer* red) {
+                        const Traj& tr, const admm_batch_reducer* red, int path) {
     namespace g = admm::gen;
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
@@ -639,8 +729,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     };
     // CU-resident solve (admm_resident.hip): anisotropic, no dim-2 spectra or isotropic norms recorded; it
     // forms the first line spectrum itself, so PREP only produces H^T y
-    const bool res = !iso && !tr.v && !tr.nrm && !tr.m && opt(ADMM_OPT_RESIDENT) != 0 && opt(ADMM_OPT_SMOOTH) != 0 &&
-                     admm::rs::has_shape(M, N, opt(ADMM_OPT_RESIDENT) >= 2);
+    const bool res = path == ADMM_PATH_RESIDENT;   // plan_paths
     // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
     if (!res || kh > 0) {
         rc = line_fwd(y, spec0);
@@ -952,9 +1041,10 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rec_forget(workspace);   // whatever was recorded there is overwritten now
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
     const size_t MN = (size_t)M * N;
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false});
     for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
         rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
-                         maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red);
+                         maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red, pl.fwd);
     int rc2 = ln.finish();
     return rc ? rc : rc2;
 }
@@ -978,22 +1068,20 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
         return fail(ADMM_E_INVALID, "x_bar must be a 16-byte aligned device pointer");
     const size_t planes = (size_t)P * B;
     if (planes > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
-    const bool want_h = (phases == 1 ? (rec_flags & ADMM_REC_HBAR) != 0 : h_bar != nullptr) && kh > 0;
-    // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
-    const bool ln_traj = fused_shape(M, N, iso != 0) && fused_enabled() && !want_h;
-    // mask-bit trajectory (ADMM_REC_MASKS, fused forward + fused reverse sweep): asked for by a recording,
-    // and taken by the combined call whenever rho_bar is not wanted
-    // isotropic at 256 x 256: the split-iteration fused forward records s and |s| lane-native for the fused
-    // reverse sweep (plane_iso.hip) -- also without rho_bar, so the same flag selects it
-    const bool iso_ok = iso && fused_tables_shape(M, N) && !want_h && fused_enabled() && fused_adj_enabled();
-    const bool masks_ok = (ln_traj && !iso && fused_adj_enabled()) || iso_ok;
-    bool use_masks = masks_ok && (phases == 1 ? (rec_flags & ADMM_REC_MASKS) != 0 : rho_bar == nullptr);
+    // the plan (plan_paths): a replay (phase 2) is planned as the recording it replays was (its flags are in
+    // the recording's tag; a replay whose options or arguments differ is rejected below)
+    int pflags = rec_flags;
     if (phases == 2) {
         std::lock_guard<std::mutex> lk(g_rec_mu);
         auto it = g_rec.find(workspace);
-        use_masks = it != g_rec.end() && it->second.masks != 0;
+        pflags = (h_bar != nullptr ? ADMM_REC_HBAR : 0) | (it != g_rec.end() && it->second.masks ? ADMM_REC_MASKS : 0);
     }
-    const bool iso_lane = use_masks && iso;   // the fused isotropic sweep (no mask bits: s itself is needed)
+    const PathPlan plan = plan_paths({M, N, iso != 0, kh > 0, phases == 3 ? ADMM_MODE_BACKWARD : ADMM_MODE_RECORD, pflags,
+                                  h_bar != nullptr, rho_bar != nullptr});
+    const bool want_h = plan.want_h;
+    const bool ln_traj = plan.ln_traj;
+    const bool use_masks = plan.masks;
+    const bool iso_lane = plan.iso_lane;   // the fused isotropic sweep (no mask bits: s itself is needed)
     const BwdLayout bl = make_bwd_layout(M, N, planes, kh, kw, maxit, want_h, iso != 0, use_masks && !iso);
     rc = check_ws(workspace, workspace_bytes, bl.total);
     if (rc) return rc;
@@ -1055,7 +1143,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     tr.sig = want_h ? reinterpret_cast<double2*>(ws + bl.sig) : nullptr;
     tr.nrm = iso ? reinterpret_cast<float*>(ws + bl.traj_n) : nullptr;
     if (phases & 1) {
-        rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, sc, iso, K, ws, bl.f, tr, red);
+        rc = run_forward(ln, y, xK, M, N, planes, h, kh, kw, sc, iso, K, ws, bl.f, tr, red, plan.fwd);
         if (rc) return rc;
     }
     if (!(phases & 2)) return ln.finish();
@@ -1082,7 +1170,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     const size_t alds = line_lds(M, T) + 8 * 16;
     const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
     // fused reverse sweep: one workgroup per plane runs all K steps (plane256_adj_kernel)
-    const bool fused_adj = ln_traj && !iso && fused_adj_enabled();
+    const bool fused_adj = plan.bwd == ADMM_PATH_SWEEP_FUSED;
     int red_rows = K * bl.nblk_line;   // rows of (rho_bar, tau_bar) partials
     if (fused_adj) {
         namespace pk = admm::plane;
@@ -1654,10 +1742,8 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
     if ((size_t)P * B > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
-    const bool want_h = (want_hbar & ADMM_REC_HBAR) != 0 && kh > 0;
-    const bool masks = (want_hbar & ADMM_REC_MASKS) != 0 && fused_shape(M, N, iso != 0) && fused_enabled() && !want_h &&
-                       fused_adj_enabled();
-    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, want_h, iso != 0, masks).total;
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_RECORD, want_hbar, false, false});
+    *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, pl.want_h, iso != 0, pl.masks && !iso).total;
     return ADMM_OK;
 }
 
@@ -1765,6 +1851,38 @@ int admm_profile_get(int kernel_class, double* total_ms, long long* launches) {
     *total_ms = g_prof.ms[kernel_class];
     *launches = g_prof.n[kernel_class];
     return ADMM_OK;
+}
+
+int admm_query_paths(int M, int N, int iso, int kh, int mode, int flags, int want_hbar, int want_rho, int* fwd_path,
+                     int* bwd_path) {
+    if (!fwd_path || !bwd_path) return fail(ADMM_E_INVALID, "admm_query_paths: NULL output");
+    if (mode != ADMM_MODE_FORWARD && mode != ADMM_MODE_RECORD && mode != ADMM_MODE_BACKWARD)
+        return fail(ADMM_E_INVALID, "admm_query_paths: unknown mode %d", mode);
+    const int rc = check_shape(M, N, 1, 1, kh, kh, iso);
+    if (rc) return rc;
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, mode, flags, want_hbar != 0, want_rho != 0});
+    *fwd_path = pl.fwd;
+    *bwd_path = pl.bwd;
+    return ADMM_OK;
+}
+
+const char* admm_path_name(int path) {
+    switch (path) {
+        case ADMM_PATH_FUSED: return "fused";
+        case ADMM_PATH_FUSED_ISO: return "fused_iso";
+        case ADMM_PATH_2PASS: return "2pass";
+        case ADMM_PATH_2PASS_ISO: return "2pass_iso";
+        case ADMM_PATH_RESIDENT: return "resident";
+        case ADMM_PATH_SMOOTH: return "smooth";
+        case ADMM_PATH_RUNTIME: return "runtime";
+        case ADMM_PATH_SWEEP_FUSED: return "sweep_fused";
+        case ADMM_PATH_SWEEP_FUSED_ISO: return "sweep_fused_iso";
+        case ADMM_PATH_SWEEP_2PASS: return "sweep_2pass";
+        case ADMM_PATH_SWEEP_2PASS_ISO: return "sweep_2pass_iso";
+        case ADMM_PATH_SWEEP_RUNTIME: return "sweep_runtime";
+        case ADMM_PATH_SWEEP_RUNTIME_ISO: return "sweep_runtime_iso";
+        default: return "none";
+    }
 }
 
 int admm_copy_async(void* dst, const void* src, size_t bytes, void* stream) {

@@ -96,7 +96,7 @@ def parse():
     ap.add_argument("--no-merge", action="store_true",
                     help="c5: solve the Parallel branches one by one (per-branch streams) instead of one grid")
     ap.add_argument("--merge-iso", action="store_true",
-                    help="c5 --iso: the branches in one grid (ADMM_MULTI_ISO) instead of one stream each")
+                    help="c5 --iso: the branches in one grid (ADMM_MULTI_ISO) at any batch (default: only when all their planes fit one wave of workgroups, layers.ISO_MERGE_MAX_PLANES)")
     ap.add_argument("--iso", action="store_true",
                     help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
     return ap.parse_args()

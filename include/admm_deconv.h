@@ -248,6 +248,33 @@ enum {
 int admm_set_option(int option, int value);
 int admm_get_option(int option, int* value);
 
+/* Which kernels a call runs (one decision table in admm_capi.hip, plan_paths; measurement and tests only).
+ * mode: ADMM_MODE_FORWARD (admm_tvd_forward_*), ADMM_MODE_RECORD (admm_tvd_forward_record_*; flags =
+ * its ADMM_REC_* word; its replay runs the sweep returned here), ADMM_MODE_BACKWARD (admm_tvd_backward_*;
+ * want_hbar / want_rho = h_bar / rho_bar non-NULL).  kh = 0: no PSF.  *fwd_path = the forward's ADMM_PATH_*,
+ * *bwd_path = the reverse sweep's ADMM_PATH_SWEEP_* (0 for a plain forward).  The current library options
+ * (admm_set_option) are taken into account; no GPU is touched.  The multi-branch entry points are not
+ * covered (one grid of the fused kernels, or ADMM_E_UNSUPPORTED). */
+enum { ADMM_MODE_FORWARD = 0, ADMM_MODE_RECORD = 1, ADMM_MODE_BACKWARD = 2 };
+enum {
+    ADMM_PATH_FUSED = 1,              /* 256 x 256 anisotropic: plane256_kernel, one launch per solve         */
+    ADMM_PATH_FUSED_ISO = 2,          /* 256 x 256 isotropic: plane256_iso_kernel + iso_norm_kernel / iter    */
+    ADMM_PATH_2PASS = 3,              /* other power-of-two shapes: column_kernel + line_kernel per iteration */
+    ADMM_PATH_2PASS_ISO = 4,          /* power-of-two isotropic: column + iso_a / iso_r / iso_b               */
+    ADMM_PATH_RESIDENT = 5,           /* smooth squares <= 256: resident_kernel, one launch per solve         */
+    ADMM_PATH_SMOOTH = 6,             /* compile-time plans for a smooth length (admm_smooth.hip)             */
+    ADMM_PATH_RUNTIME = 7,            /* runtime plans for any length (admm_generic.hip)                      */
+    ADMM_PATH_SWEEP_FUSED = 8,        /* plane256_adj_kernel, one launch per sweep                            */
+    ADMM_PATH_SWEEP_FUSED_ISO = 9,    /* plane256_isoadj_kernel + iso_radj_kernel per step                   */
+    ADMM_PATH_SWEEP_2PASS = 10,       /* line_adj + column per step                                          */
+    ADMM_PATH_SWEEP_2PASS_ISO = 11,   /* iso_adj_a / _r / _b + column per step                                */
+    ADMM_PATH_SWEEP_RUNTIME = 12,     /* admm_generic_bwd.hip                                                 */
+    ADMM_PATH_SWEEP_RUNTIME_ISO = 13
+};
+int admm_query_paths(int M, int N, int iso, int kh, int mode, int flags, int want_hbar, int want_rho, int* fwd_path,
+                     int* bwd_path);
+const char* admm_path_name(int path);
+
 /* Output transport of the batch-sharded solve (BASELINE c3; the reference gathers nothing -- its batch
  * lives on one device, ops.jl:168-173): an asynchronous copy of `bytes` from src to dst on `stream`, both
  * device pointers, dst possibly memory of another GPU opened through a HIP IPC handle.  A plain

@@ -1,0 +1,43 @@
+"""The path every (shape, prox, PSF, call, record flags, options) combination must take -- the expected side of
+admm_query_paths (admm_capi.hip plan_paths, the library's one decision table).  Shared by the CPU test
+(tests/test_capi.py: the table against the query) and the GPU test (tests/test_gpu_paths.py: the kernels that
+actually launch against the table).  mode: 0 forward, 1 record (flags = ADMM_REC_*), 2 combined backward."""
+
+HBAR, MASKS = 1, 2
+F, R, B = 0, 1, 2
+
+# (id, M, N, iso, kh, mode, flags, want_hbar, want_rho, options, expected forward, expected sweep)
+CASES = [
+    ("c2-forward", 256, 256, False, 15, F, 0, False, False, {}, "fused", None),
+    ("c2-forward-FUSED0", 256, 256, False, 15, F, 0, False, False, {"FUSED": 0}, "2pass", None),
+    ("iso256-forward", 256, 256, True, 15, F, 0, False, False, {}, "fused_iso", None),
+    ("iso256-forward-FUSED0", 256, 256, True, 15, F, 0, False, False, {"FUSED": 0}, "2pass_iso", None),
+    ("c4-forward", 512, 512, False, 15, F, 0, False, False, {}, "2pass", None),
+    ("iso512-forward", 512, 512, True, 0, F, 0, False, False, {}, "2pass_iso", None),
+    ("250-forward", 250, 250, False, 15, F, 0, False, False, {}, "resident", None),
+    ("240-forward", 240, 240, False, 15, F, 0, False, False, {}, "resident", None),
+    ("96-forward", 96, 96, False, 0, F, 0, False, False, {}, "resident", None),
+    ("250-forward-RESIDENT0", 250, 250, False, 15, F, 0, False, False, {"RESIDENT": 0}, "smooth", None),
+    ("250-forward-SMOOTH0", 250, 250, False, 15, F, 0, False, False, {"SMOOTH": 0}, "runtime", None),
+    ("250-iso-forward", 250, 250, True, 15, F, 0, False, False, {}, "smooth", None),
+    ("480x640-forward", 640, 480, False, 15, F, 0, False, False, {}, "smooth", None),
+    ("primes-forward", 37, 29, False, 5, F, 0, False, False, {}, "runtime", None),
+    # c5 layers: ADMMDeconvF2 (lambda trainable, rho fixed) records mask bits / the lane-native iso trajectory
+    ("c5-record-masks", 256, 256, False, 0, R, MASKS, False, False, {}, "fused", "sweep_fused"),
+    ("c5-record-full", 256, 256, False, 0, R, 0, False, False, {}, "fused", "sweep_fused"),
+    ("c5-record-FUSED_ADJ0", 256, 256, False, 0, R, MASKS, False, False, {"FUSED_ADJ": 0}, "fused", "sweep_2pass"),
+    ("c5iso-record-masks", 256, 256, True, 0, R, MASKS, False, False, {}, "fused_iso", "sweep_fused_iso"),
+    ("c5iso-record-full", 256, 256, True, 0, R, 0, False, False, {}, "2pass_iso", "sweep_2pass_iso"),
+    ("256-record-hbar", 256, 256, False, 15, R, HBAR, False, False, {}, "2pass", "sweep_2pass"),
+    ("256-record-hbar-masks", 256, 256, False, 15, R, HBAR | MASKS, False, False, {}, "2pass", "sweep_2pass"),
+    ("256-backward-norho", 256, 256, False, 15, B, 0, False, False, {}, "fused", "sweep_fused"),
+    ("256-backward-rho", 256, 256, False, 15, B, 0, False, True, {}, "fused", "sweep_fused"),
+    ("256-backward-hbar", 256, 256, False, 15, B, 0, True, True, {}, "2pass", "sweep_2pass"),
+    ("iso256-backward-norho", 256, 256, True, 15, B, 0, False, False, {}, "fused_iso", "sweep_fused_iso"),
+    ("iso256-backward-rho", 256, 256, True, 15, B, 0, False, True, {}, "2pass_iso", "sweep_2pass_iso"),
+    ("c4-backward", 512, 512, False, 15, B, 0, True, True, {}, "2pass", "sweep_2pass"),
+    ("250-record", 250, 250, False, 15, R, 0, False, False, {}, "resident", "sweep_runtime"),
+    ("250-record-hbar", 250, 250, False, 15, R, HBAR, False, False, {}, "smooth", "sweep_runtime"),
+    ("250-iso-backward", 250, 250, True, 15, B, 0, True, True, {}, "smooth", "sweep_runtime_iso"),
+    ("primes-backward", 37, 29, False, 5, B, 0, True, True, {}, "runtime", "sweep_runtime"),
+]

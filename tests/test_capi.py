@@ -195,3 +195,16 @@ def test_multi_branch_workspace_and_validation():
     # the single-solve isotropic recording without rho_bar (the fused sweep) keeps the full-size trajectory
     fi = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, True, 50, 0)
     assert _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, True, 50, _lib.REC_MASKS) == fi
+
+
+@pytest.mark.parametrize("case", __import__("paths_table").CASES, ids=[c[0] for c in __import__("paths_table").CASES])
+def test_path_decision_table(case):
+    """Every (shape, prox, PSF, call, record flags, options) combination takes its intended path: the library's
+    one decision table (admm_capi.hip plan_paths) answered through admm_query_paths, host code only.
+    tests/test_gpu_paths.py checks on the GPU that these are the kernels that launch."""
+    import contextlib
+    cid, M, N, iso, kh, mode, flags, hb, rho, opts, fwd, bwd = case
+    with contextlib.ExitStack() as st:
+        for k, v in opts.items():
+            st.enter_context(_lib.option(k, v))
+        assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho) == (fwd, bwd), cid

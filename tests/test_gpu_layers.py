@@ -66,6 +66,26 @@ def test_creg_clamp(dev):
     assert abs(L.lam.item() - 0.01) < 1e-7 and abs(L.rho.item() - 0.01) < 1e-7
 
 
+def test_parallel_merges_isotropic_branches_only_within_one_wave(dev):
+    """Default merge rule (layers.ISO_MERGE_MAX_PLANES): anisotropic branches always share one grid; isotropic ones
+    when all their planes fit one wave of workgroups -- the reference's training batch (batch_size 2, RGB, 5
+    branches: 30 planes, src/configs/train_cfg.json:10-14) merges, 18 RGB images (270 planes) do not -- unless
+    merge="always"."""
+    from admm_deconv import layers
+    rng = np.random.default_rng(1)
+    for iso in (False, True):
+        branch = [layers.ADMMDeconvF2((), 5, r, layers.relu1, iso=iso, rng=rng, device=dev)
+                  for r in (0.002, 0.02, 0.2, 2.0, 4.0)]
+        for L in branch:
+            L.lam.requires_grad_(True)
+        small = torch.zeros(2, 3, 256, 256, device=dev)
+        big = torch.zeros(18, 3, 256, 256, device=dev)
+        auto = layers.Parallel(layers.chcat, *branch)
+        assert auto._mergeable(small)
+        assert auto._mergeable(big) == (not iso)
+        assert layers.Parallel(layers.chcat, *branch, merge="always")._mergeable(big)
+
+
 @pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])
 @pytest.mark.parametrize("train_rho", [False, True], ids=["lam", "lam+rho"])
 def test_parallel_branches_on_streams_match_serial(dev, train_rho, iso):
