@@ -206,8 +206,10 @@ def chcat(*xs):
     return torch.cat(xs, dim=1)
 
 
-# isotropic branches are merged into one grid by default when all their planes fit one wave of workgroups
-ISO_MERGE_MAX_PLANES = 256
+# isotropic branches are merged into one grid by default up to this many planes in all (c5 iso, 5 branches of
+# 3-channel images: 30 planes 229 vs 119 img/s, 120: 730 vs 431, 240: 954 vs 740, 480: 984 vs 980, 960: 1027
+# vs 1111 merged vs per-branch streams; profiles/r04_c5_configs.jsonl, profiles/r04_c5iso_merge.jsonl)
+ISO_MERGE_MAX_PLANES = 512
 
 
 class Parallel:
@@ -239,13 +241,13 @@ class Parallel:
         if not all(isinstance(L, Admm) for L in Ls):
             return False
         K, iso = Ls[0].iters, Ls[0].iso
-        # isotropic: its one-grid solve is a launch per iteration either way.  When every branch's planes together
-        # fit one wave of workgroups (<= ISO_MERGE_MAX_PLANES, one plane per CU), one grid per iteration halves the
-        # launches and the chip is not full anyway: the reference's training batch (train_cfg.json batch_size 2,
-        # 5 branches x 6 planes) runs 229 img/s merged against 119 per-branch.  Above that, the branches on their
-        # own streams overlap one branch's batch-norm launches with the others' plane launches: batch 64 (960
-        # planes) 1.11k img/s per-branch against 1.03k merged (profiles/r04_c5_configs.jsonl).  merge="always"
-        # merges at any size.  The merged grid forms no rho_bar.
+        # isotropic: its one-grid solve is a launch per iteration either way.  Up to ISO_MERGE_MAX_PLANES planes in
+        # all (about two waves of workgroups, one plane per CU), one grid per iteration halves the launches and
+        # fills the chip better: the reference's training batch (train_cfg.json batch_size 2, 5 branches x 6
+        # planes) runs 229 img/s merged against 119 per-branch.  Above that, the branches on their own streams
+        # overlap one branch's batch-norm launches with the others' plane launches: batch 64 (960 planes) 1.11k
+        # img/s per-branch against 1.03k merged.  merge="always" merges at any size.  The merged grid forms no
+        # rho_bar.
         if iso:
             if any(self._needs_rho(L) for L in Ls):
                 return False

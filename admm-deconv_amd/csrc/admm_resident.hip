@@ -43,7 +43,7 @@ using sm::SP;
 
 constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
 #ifndef RS_PD
-#define RS_PD 3                           // rows of update loads in flight ahead of the row being computed
+#define RS_PD 4                           // rows of update loads in flight ahead of the row being computed
 #endif
 #ifndef RS_RAD
 #define RS_RAD 16
@@ -255,13 +255,25 @@ struct Geo {
     static constexpr int nr(int n) { return cdiv(NN, ls(n)); }
     static constexpr int fs(int n) { return (nr(n) * ls(n)) | 1; }
     static constexpr bool fits(int n) { return ls(n) >= 2 && kbc(n) * fs(n) <= kBudget; }
-    static constexpr int ncc() {   // fewest spectrum registers, then fewest chunks
-        int best = 0;
+    // fewest chunks whose spectrum takes at most 2 registers more than the fewest possible: every chunk is a
+    // round of column passes with its barriers (250^2: 2 chunks of 32 registers, not 3 of 21; 85.0k vs 84.0k
+    // img/s, profiles/r04_resident_variants.txt)
+    static constexpr int min_regs() {
+        int m = 1 << 30;
         for (int n = 1; n <= 8 && n <= H; ++n)
-            if (fits(n) && (best == 0 || n * nr(n) < best * nr(best))) best = n;
-        return best;
+            if (fits(n) && n * nr(n) < m) m = n * nr(n);
+        return m;
     }
+    static constexpr int ncc() {
+        for (int n = 1; n <= 8 && n <= H; ++n)
+            if (fits(n) && n * nr(n) <= min_regs() + 2) return n;
+        return 0;
+    }
+#ifdef RS_NCC_FORCE   // experiments: column chunk count forced
+    static constexpr int NCC = fits(RS_NCC_FORCE) ? RS_NCC_FORCE : ncc();
+#else
     static constexpr int NCC = ncc();              // column chunks
+#endif
     static constexpr int KBC = kbc(NCC);           // bins per column chunk
     static constexpr int LS = ls(NCC);             // line slots
     static constexpr int NR = nr(NCC);             // registers per column chunk

@@ -67,10 +67,9 @@ def test_creg_clamp(dev):
 
 
 def test_parallel_merges_isotropic_branches_only_within_one_wave(dev):
-    """Default merge rule (layers.ISO_MERGE_MAX_PLANES): anisotropic branches always share one grid; isotropic ones
-    when all their planes fit one wave of workgroups -- the reference's training batch (batch_size 2, RGB, 5
-    branches: 30 planes, src/configs/train_cfg.json:10-14) merges, 18 RGB images (270 planes) do not -- unless
-    merge="always"."""
+    """Default merge rule (layers.ISO_MERGE_MAX_PLANES = 512): anisotropic branches always share one grid; isotropic
+    ones up to 512 planes in all -- the reference's training batch (batch_size 2, RGB, 5 branches: 30 planes,
+    src/configs/train_cfg.json:10-14) merges, 36 RGB images (540 planes) do not -- unless merge="always"."""
     from admm_deconv import layers
     rng = np.random.default_rng(1)
     for iso in (False, True):
@@ -79,7 +78,7 @@ def test_parallel_merges_isotropic_branches_only_within_one_wave(dev):
         for L in branch:
             L.lam.requires_grad_(True)
         small = torch.zeros(2, 3, 256, 256, device=dev)
-        big = torch.zeros(18, 3, 256, 256, device=dev)
+        big = torch.zeros(36, 3, 256, 256, device=dev)
         auto = layers.Parallel(layers.chcat, *branch)
         assert auto._mergeable(small)
         assert auto._mergeable(big) == (not iso)

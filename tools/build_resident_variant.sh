@@ -11,6 +11,7 @@ mkdir -p $O
 python3 -c "
 import sys; sys.path.insert(0, '$C'); import hazard_pad
 hazard_pad.compile_tu('$C/admm_resident.hip', '$O/admm_resident.o',
-    ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Xclang', '-target-feature', '-Xclang', '-packed-fp32-ops'] + sys.argv[1:])" "$@"
+    ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-Xclang', '-target-feature', '-Xclang', '-packed-fp32-ops',
+     '-mllvm', '-structurizecfg-skip-uniform-regions=true'] + sys.argv[1:])" "$@"
 hipcc --offload-arch=gfx950 -fPIC -shared -o $R/admm-deconv_amd/libadmm_deconv_$TAG.so $C/admm_capi.o $C/plane_launch.o $C/admm_smooth.o $O/admm_resident.o $C/metrics_capi.o
 echo built $TAG
