@@ -152,3 +152,22 @@ def test_bench_two_ranks_gloo(dev):
         assert r["ms_per_step"] > 0 and r["solve_only_ms_per_step"] > 0 and r["gather_tail_ms"] >= 0
         assert r["device"] == 0 and r["visible_devices"] >= 1
     assert d["solve_only"]["value"] > 0 and d["solve_only"]["ms_per_step"] > 0
+
+
+def test_copy_async_is_a_stream_ordered_device_copy(dev):
+    """admm_copy_async (the IPC gather's peer copy, include/admm_deconv.h): a hipMemcpyAsync on the given stream,
+    ordered after earlier work on that stream and before later work; NULL pointers are rejected; 0 bytes is a
+    no-op."""
+    from admm_deconv import _lib
+    src = torch.arange(1 << 20, dtype=torch.float32, device=dev)
+    dst = torch.zeros_like(src)
+    st = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(st):
+        src.mul_(2.0)                                         # earlier work on st
+        _lib.copy_async(dst.data_ptr(), src.data_ptr(), src.numel() * 4, st.cuda_stream)
+        dst.add_(1.0)                                         # later work on st
+    st.synchronize()
+    assert torch.equal(dst, torch.arange(1 << 20, dtype=torch.float32, device=dev) * 2 + 1)
+    _lib.copy_async(dst.data_ptr(), src.data_ptr(), 0, st.cuda_stream)
+    with pytest.raises(_lib.AdmmError):
+        _lib.copy_async(0, src.data_ptr(), 4, st.cuda_stream)
