@@ -391,9 +391,12 @@ struct FwdRule {
 const FwdRule kFwdRules[] = {
     // runtime-length shapes: the CU-resident solve (admm_resident.hip) where compiled and measured faster,
     // anisotropic and recording neither dim-2 spectra, norms nor mask bits (it writes s_k into the slots)
+    // (and the small power-of-two squares it compiled: 32, 64, 128; it needs no spectra buffers, so it runs on
+    // either layout)
     {ADMM_PATH_RESIDENT, [](const PathIn& q, const TrajFlags& t) {
-         return generic_shape(q.M, q.N) && !q.iso && !t.v && !t.nrm && !t.m && opt(ADMM_OPT_RESIDENT) != 0 &&
-                opt(ADMM_OPT_SMOOTH) != 0 && admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
+         return !q.iso && !t.v && !t.nrm && !t.m && opt(ADMM_OPT_RESIDENT) != 0 &&
+                (!generic_shape(q.M, q.N) || opt(ADMM_OPT_SMOOTH) != 0) &&
+                admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
      }},
     // compile-time-plan kernels when this build has either length (admm_smooth.hip), else runtime plans
     {ADMM_PATH_SMOOTH, [](const PathIn& q, const TrajFlags&) {
@@ -539,7 +542,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     }
 
     const int path = fwd_path;
-    if (path == ADMM_PATH_RESIDENT || path == ADMM_PATH_SMOOTH || path == ADMM_PATH_RUNTIME) {
+    if (generic_shape(M, N)) {   // ADMM_PATH_RESIDENT (smooth sides), _SMOOTH, _RUNTIME: the runtime-length layout
         return run_forward_generic(ln, y, x_out, M, N, planes, kh, iso, maxit, ws, lay, tr, red, path);
     }
     if (path == ADMM_PATH_FUSED) {
@@ -604,6 +607,23 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
     const size_t np = planes;
     const dim3 gl(N / T, (unsigned)np), gc(L / KB, (unsigned)np);
+    if (path == ADMM_PATH_RESIDENT) {
+        // power-of-two sides admm_resident.hip compiled: one workgroup per plane runs all K iterations (s_k into
+        // the trajectory slots when recording, natural layout, as the 2-pass sweep reads them); H^T y from the
+        // 2-pass PREP kernels (line, column x conj(Sigma_c), line), the first line spectrum formed in the kernel
+        if (kh > 0) {
+            rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_PREP, [&] { return launch_column(N, 1, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f); });
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_PREP, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
+            if (rc) return rc;
+        }
+        return ln.run(ADMM_K_PLANE, [&] {
+            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, np * 2 * MN, x_out, Ct, twM, twN, prm,
+                                    maxit, opt(ADMM_OPT_PLANE_STAGGER));
+        });
+    }
     // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
     rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
     if (rc) return rc;

@@ -737,17 +737,20 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 }
 
 // ---- host side -----------------------------------------------------------------------------------------------
-// Shapes compiled here (M = line length, N = lines): square smooth sides the 2-pass path serves
+// Shapes compiled here (M = line length, N = lines): square smooth sides the 2-pass path serves, and the small
+// power-of-two squares (the reference's 32 x 32 demo crops, src/ADMM_Deconv.jl:17-23; 64, 128)
 #ifndef RS_SHAPES_OVERRIDE
-#define RS_SHAPES(X) X(250, 250) X(240, 240) X(200, 200) X(192, 192) X(160, 160) X(120, 120) X(96, 96)
+#define RS_SHAPES(X) \
+    X(250, 250) X(240, 240) X(200, 200) X(192, 192) X(160, 160) X(128, 128) X(120, 120) X(96, 96) X(64, 64) X(32, 32)
 #else
 #define RS_SHAPES(X) RS_SHAPES_OVERRIDE(X)
 #endif
 
 // Compiled shapes where the 2-pass smooth kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the
-// 2-pass path; 2 forces the resident kernel on every compiled shape).  None since the spills went (round 4:
-// 240^2 resident 77.8k img/s vs 74.2k 2-pass, profiles/r04_resident_shapes.jsonl).
-#define RS_SLOWER(X)
+// 2-pass path; 2 forces the resident kernel on every compiled shape).  No smooth shape since the spills went
+// (round 4: 240^2 resident 77.8k img/s vs 74.2k 2-pass, profiles/r04_resident_shapes.jsonl); the power-of-two
+// squares until measured against their tuned 2-pass kernels.
+#define RS_SLOWER(X) X(128, 128) X(64, 64) X(32, 32)
 
 bool has_shape(int M, int N, bool all) {
 #define X(m, n) \

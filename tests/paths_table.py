@@ -22,6 +22,11 @@ CASES = [
     ("250-iso-forward", 250, 250, True, 15, F, 0, False, False, {}, "smooth", None),
     ("480x640-forward", 640, 480, False, 15, F, 0, False, False, {}, "smooth", None),
     ("primes-forward", 37, 29, False, 5, F, 0, False, False, {}, "runtime", None),
+    ("128-forward", 128, 128, False, 15, F, 0, False, False, {}, "2pass", None),
+    ("128-forward-RESIDENT2", 128, 128, False, 15, F, 0, False, False, {"RESIDENT": 2}, "resident", None),
+    ("demo32-record-RESIDENT2", 32, 32, False, 32, R, 0, False, False, {"RESIDENT": 2}, "resident", "sweep_2pass"),
+    ("demo32-record-hbar-RESIDENT2", 32, 32, False, 32, R, HBAR, False, False, {"RESIDENT": 2}, "2pass", "sweep_2pass"),
+    ("64-iso-RESIDENT2", 64, 64, True, 0, F, 0, False, False, {"RESIDENT": 2}, "2pass_iso", None),
     # c5 layers: ADMMDeconvF2 (lambda trainable, rho fixed) records mask bits / the lane-native iso trajectory
     ("c5-record-masks", 256, 256, False, 0, R, MASKS, False, False, {}, "fused", "sweep_fused"),
     ("c5-record-full", 256, 256, False, 0, R, 0, False, False, {}, "fused", "sweep_fused"),

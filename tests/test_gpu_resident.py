@@ -29,6 +29,10 @@ CASES = [
     (2, 1, 160, 160, None, 0.05, 0.1, 6),
     (3, 1, 120, 120, ("gauss", 15, 2.5), 0.0041, 0.021, 8),    # one line chunk: halo pairs are its own lines
     (4, 1, 96, 96, ("gauss", 9, 1.5), 0.0041, 0.021, 25),
+    # power-of-two squares (round 4; the 2-pass PREP on the power-of-two layout, then the resident solve)
+    (2, 1, 128, 128, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
+    (2, 3, 64, 64, None, 0.02, 0.02, 12),
+    (2, 3, 32, 32, ("rand", 32, 32), 0.0005, 0.3, 50),          # the reference demo (src/ADMM_Deconv.jl:17-23)
 ]
 
 
@@ -88,13 +92,15 @@ def test_resident_deterministic_and_batch_invariant(dev):
     assert torch.equal(a, part), "planes are independent (ops.jl:168-173): sub-batches give the same planes"
 
 
-def test_resident_recorded_gradients_match_2pass(dev):
-    """Training at a smooth size: the recording forward runs resident (s_k into the trajectory slots), the
-    reverse sweep is the 2-pass adjoint.  Gradients against the all-2-pass recording within fp32 rounding."""
+@pytest.mark.parametrize("side,res", [(250, 1), (128, 2)], ids=["250", "128-pow2"])
+def test_resident_recorded_gradients_match_2pass(dev, side, res):
+    """Training at a smooth (or small power-of-two) size: the recording forward runs resident (s_k into the
+    trajectory slots), the reverse sweep is the 2-pass adjoint.  Gradients against the all-2-pass recording
+    within fp32 rounding."""
     h = synth.gaussian_psf(9, 1.5)
-    yb = synth.make_batch(2, 250, 250, h, g0=3)
+    yb = synth.make_batch(2, side, side, h, g0=3)
     out = {}
-    for res in (1, 0):
+    for res in (res, 0):
         with _lib.option("RESIDENT", res):
             y = torch.from_numpy(yb).to(dev).requires_grad_(True)
             lam = torch.tensor([0.0041], device=dev, requires_grad=True)
@@ -102,7 +108,8 @@ def test_resident_recorded_gradients_match_2pass(dev):
             (x * x).sum().backward()
             torch.cuda.synchronize()
             out[res] = (x.detach().cpu().numpy(), y.grad.cpu().numpy(), float(lam.grad))
+    r = max(out)
     for i, what in ((0, "x"), (1, "y_bar")):
-        d = np.linalg.norm((out[1][i] - out[0][i]).ravel()) / np.linalg.norm(out[0][i].ravel())
+        d = np.linalg.norm((out[r][i] - out[0][i]).ravel()) / np.linalg.norm(out[0][i].ravel())
         assert d < 1e-5, f"{what}: resident recording vs 2-pass rel-L2 {d:.2e}"
-    assert abs(out[1][2] - out[0][2]) <= 1e-4 * abs(out[0][2]), (out[1][2], out[0][2])
+    assert abs(out[r][2] - out[0][2]) <= 1e-4 * abs(out[0][2]), (out[r][2], out[0][2])
