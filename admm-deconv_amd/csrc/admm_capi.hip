@@ -398,6 +398,12 @@ const FwdRule kFwdRules[] = {
                 (!generic_shape(q.M, q.N) || opt(ADMM_OPT_SMOOTH) != 0) &&
                 admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
      }},
+    // isotropic: the split-iteration CU-resident solve (resident_iso_kernel, one launch per iteration with the
+    // norm kernel between); it records s_k and |s_k| in the natural layout the 2-pass / runtime sweeps read
+    {ADMM_PATH_RESIDENT_ISO, [](const PathIn& q, const TrajFlags& t) {
+         return q.iso && !t.v && opt(ADMM_OPT_RESIDENT) != 0 && (!generic_shape(q.M, q.N) || opt(ADMM_OPT_SMOOTH) != 0) &&
+                admm::rs::has_iso_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
+     }},
     // compile-time-plan kernels when this build has either length (admm_smooth.hip), else runtime plans
     {ADMM_PATH_SMOOTH, [](const PathIn& q, const TrajFlags&) {
          return generic_shape(q.M, q.N) && opt(ADMM_OPT_SMOOTH) != 0 &&
@@ -508,6 +514,47 @@ int call_reducer(const admm_batch_reducer* red, float* buf, size_t count, hipStr
     return ADMM_OK;
 }
 
+// Isotropic CU-resident solve (ADMM_PATH_RESIDENT_ISO): iteration k is one resident_iso_kernel launch (s_k, f_k ->
+// s_{k+1}, q per plane; x at the last), then the 2-pass path's norm over the planes' q (iso_r, or for a sharded
+// batch the shard sum, the caller's all-reduce and the factor) -> f_{k+1} (and |s_{k+1}| when recording).
+// Recording: s_{k+1} into trajectory slot k, read back from slot k - 1 -- the natural layout the 2-pass and
+// runtime-length isotropic sweeps read.  q: planes x M x N floats (a spectrum buffer, free after PREP).
+int run_resident_iso(Launcher& ln, int M, int N, size_t planes, const float* hty, float* sbuf0, float* q, float* fmap,
+                     float* x_out, const float* Ct, const float2* twM, const float2* twN, const float* prm, int maxit,
+                     const Traj& tr, const admm_batch_reducer* red) {
+    hipStream_t s = ln.s;
+    const size_t MN = (size_t)M * N, sstride = planes * 2 * MN;
+    const int nb = (int)((MN + 63) / 64);   // 64 pixels per block (group_sum)
+    const dim3 gr(nb < 2048 ? nb : 2048);
+    for (int k = 0; k < maxit; ++k) {
+        const float* sin = tr.s && k >= 1 ? tr.s + (size_t)(k - 1) * sstride : sbuf0;
+        float* sout = tr.s ? tr.s + (size_t)k * sstride : sbuf0;
+        int rc = ln.run(ADMM_K_PLANE, [&] {
+            return admm::rs::launch_iso(M, N, planes, s, hty, sin, sout, fmap, q, x_out, Ct, twM, twN, prm, k, maxit);
+        });
+        if (rc) return rc;
+        if (k + 1 == maxit) break;
+        float* nrm_out = tr.nrm ? tr.nrm + (size_t)k * MN : nullptr;
+        if (red) {
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_sum_kernel, gr, dim3(kThreads), 0, s, q, fmap, (int)planes, MN);
+            });
+            if (rc) return rc;
+            rc = call_reducer(red, fmap, MN, s);
+            if (rc) return rc;
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_fin_kernel, gr, dim3(kThreads), 0, s, fmap, MN, prm, nrm_out);
+            });
+        } else {
+            rc = ln.run(ADMM_K_NORM, [&] {
+                hipLaunchKernelGGL(admm::iso_r_kernel, gr, dim3(kThreads), 0, s, q, fmap, (int)planes, MN, prm, nrm_out);
+            });
+        }
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
                 int kw, const admm::ScalarSrc& sc, int iso, int maxit, unsigned char* ws, const Layout& lay,
                 const Traj& tr, const admm_batch_reducer* red, int fwd_path) {
@@ -607,7 +654,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
     const size_t np = planes;
     const dim3 gl(N / T, (unsigned)np), gc(L / KB, (unsigned)np);
-    if (path == ADMM_PATH_RESIDENT) {
+    if (path == ADMM_PATH_RESIDENT || path == ADMM_PATH_RESIDENT_ISO) {
         // power-of-two sides admm_resident.hip compiled: one workgroup per plane runs all K iterations (s_k into
         // the trajectory slots when recording, natural layout, as the 2-pass sweep reads them); H^T y from the
         // 2-pass PREP kernels (line, column x conj(Sigma_c), line), the first line spectrum formed in the kernel
@@ -619,6 +666,9 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
             rc = ln.run(ADMM_K_PREP, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
             if (rc) return rc;
         }
+        if (path == ADMM_PATH_RESIDENT_ISO)
+            return run_resident_iso(ln, M, N, planes, hty, sbuf[0], reinterpret_cast<float*>(spec1), fmap, x_out, Ct, twM,
+                                    twN, prm, maxit, tr, red);
         return ln.run(ADMM_K_PLANE, [&] {
             return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, np * 2 * MN, x_out, Ct, twM, twN, prm,
                                     maxit, opt(ADMM_OPT_PLANE_STAGGER));
@@ -749,7 +799,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     };
     // CU-resident solve (admm_resident.hip): anisotropic, no dim-2 spectra or isotropic norms recorded; it
     // forms the first line spectrum itself, so PREP only produces H^T y
-    const bool res = path == ADMM_PATH_RESIDENT;   // plan_paths
+    const bool res = path == ADMM_PATH_RESIDENT || path == ADMM_PATH_RESIDENT_ISO;   // plan_paths
     // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
     if (!res || kh > 0) {
         rc = line_fwd(y, spec0);
@@ -775,6 +825,9 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     }
     const int ng = iso_ngroups(planes);
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
+    if (path == ADMM_PATH_RESIDENT_ISO)
+        return run_resident_iso(ln, M, N, planes, hty, sbuf[0], reinterpret_cast<float*>(spec1), fmap, x_out, Ct, twM, twN,
+                                prm, maxit, tr, red);
     if (res) {
         return ln.run(ADMM_K_PLANE, [&] {
             return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit,
@@ -1901,6 +1954,7 @@ const char* admm_path_name(int path) {
         case ADMM_PATH_SWEEP_2PASS_ISO: return "sweep_2pass_iso";
         case ADMM_PATH_SWEEP_RUNTIME: return "sweep_runtime";
         case ADMM_PATH_SWEEP_RUNTIME_ISO: return "sweep_runtime_iso";
+        case ADMM_PATH_RESIDENT_ISO: return "resident_iso";
         default: return "none";
     }
 }

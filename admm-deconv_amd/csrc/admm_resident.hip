@@ -383,7 +383,8 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, 
 // Lines are held as complex pairs z_f = line 2f + i line 2f+1 (both spectra with their Hermitian
 // extensions folded in, then both real lines after the inverse), M float2 per pair.  Update mode stages
 // the chunk plus the halo pairs (jc0 - 2, jc0 - 1) and (jc1, jc1 + 1): pair u / 2 of staged line u.
-enum Mode { kInit = 0, kUpdate = 1, kFinal = 2 };
+// kIsoB / kIsoA: the isotropic solve's two halves of an iteration (resident_iso_kernel below)
+enum Mode { kInit = 0, kUpdate = 1, kFinal = 2, kIsoB = 3, kIsoA = 4 };
 
 struct LineArgs {
     const float* hty;     // this plane's H^T y
@@ -392,6 +393,8 @@ struct LineArgs {
     float* xo;            // x out (final)
     float tau, rho;
     bool first;
+    const float* fm;      // isotropic: the batch's BT factor map f_k (M x N, L2-resident)
+    float* q;             // isotropic: this plane's q = s1^2 + s2^2 of s_{k+1} (the batch norm's input)
 };
 
 __device__ __forceinline__ float2 lane_swap(float2 v) {   // value of lane t ^ 1 (DPP quad_perm [1, 0, 3, 2])
@@ -439,14 +442,14 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
     constexpr int LS = G::LS, P = RD::P, NR = G::NR, NCC = G::NCC, KBC = G::KBC, H = G::H;
     constexpr int jc0 = C * G::TL, jc1 = imin(NN, jc0 + G::TL), T = jc1 - jc0;
     constexpr int rc0 = jc0 / LS, rc1 = cdiv(jc1, LS);   // the chunk's registers (the last may hold lines >= NN)
-    constexpr int HP = MODE == kUpdate ? 1 : 0;   // halo pairs either side
+    constexpr int HP = (MODE == kUpdate || MODE == kIsoA) ? 1 : 0;   // halo pairs either side
     constexpr int NP = T / 2 + 2 * HP;            // pairs staged
     float2* buf = th.buf;
     float* Xf = reinterpret_cast<float*>(buf);
     const Acc<MM> al{buf};
     const bool odd = th.jt & 1;
 
-    if constexpr (MODE != kInit) {
+    if constexpr (MODE != kInit && MODE != kIsoB) {
         // ---- S -> z pairs (stores only), inverse DIF (x at dpos order) ----
         float2* zb0 = buf + (th.jt >> 1) * MM;   // + z slot + pair offset of register r
         static_for<0, NCC>([&](auto ic) {
@@ -480,6 +483,36 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         for (int idx = tid(); idx < T * MM; idx += kNT) {
             const int u = idx / MM, i = idx - u * MM;
             xo[idx] = Xf[2 * ((u >> 1) * MM + dpos<MM>(i)) + (u & 1)];
+        }
+        __syncthreads();
+        return;
+    }
+
+    if constexpr (MODE == kIsoA) {
+        // ---- isotropic A phase: s_{k+1} = D x_{k+1} + u_k, u_k = s_k - f_k s_k (z = f s, ops.jl:10; first: u = 0),
+        // stored (in place: every element is read and rewritten by its own thread), and q = s1^2 + s2^2 of the
+        // pixel for the batch norm.  x of line j - 1 (channel 0, dim 2) and pixel i - 1 (channel 1, dim 1) from
+        // the staged rows (the halo pair holds lines jc0 - 2, jc0 - 1).  No forward transform: the next launch's
+        // B phase forms the spectrum from s_{k+1}.
+        constexpr unsigned MN = (unsigned)MM * NN;
+        auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
+        for (int idx = tid(); idx < T * MM; idx += kNT) {
+            const int u = 2 + idx / MM, i = idx - (u - 2) * MM;
+            const int j = jc0 + u - 2;
+            const float xc = Xf[row(u) + 2 * dpos<MM>(i)];
+            const float xp = Xf[row(u - 1) + 2 * dpos<MM>(i)];
+            const float xl = Xf[row(u) + 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1)];
+            const unsigned e = (unsigned)j * MM + i;
+            float u0 = 0.0f, u1 = 0.0f;
+            if (!a.first) {
+                const float f = a.fm[e], o0 = a.so[e], o1 = a.so[MN + e];
+                u0 = o0 - f * o0;
+                u1 = o1 - f * o1;
+            }
+            const float s0 = (xc - xp) + u0, s1 = (xc - xl) + u1;
+            a.sn[e] = s0;
+            a.sn[MN + e] = s1;
+            a.q[e] = s0 * s0 + s1 * s1;
         }
         __syncthreads();
         return;
@@ -624,6 +657,22 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         __syncthreads();
         // ---- forward DIT of the chunk's pairs (v at dpos order -> natural z) ----
         dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, Acc<MM>{buf + MM});
+    } else if constexpr (MODE == kIsoB) {
+        // isotropic B phase: v = H^T y + rho D^T w, w = z - u = f s - (s - f s) of s_k and f_k (ops.jl:10, 168), into
+        // the pairs at dpos order (element of line jc0 + u, pixel i at float 2 ((u / 2) M + dpos(i)) + u % 2).
+        // D^T needs w of line j + 1 (channel 0) and of pixel i + 1 (channel 1): re-read, L1 / L2-served.
+        constexpr unsigned MN = (unsigned)MM * NN;
+        for (int idx = tid(); idx < T * MM; idx += kNT) {
+            const int u = idx / MM, i = idx - u * MM;
+            const int j = jc0 + u, jn = j + 1 == NN ? 0 : j + 1, ir = i + 1 == MM ? 0 : i + 1;
+            const unsigned e = (unsigned)j * MM + i, en = (unsigned)jn * MM + i, er = (unsigned)j * MM + ir;
+            auto wof = [](float f, float sv) { return f * sv - (sv - f * sv); };
+            const float w0 = wof(a.fm[e], a.so[e]), w0n = wof(a.fm[en], a.so[en]);
+            const float w1 = wof(a.fm[e], a.so[MN + e]), w1r = wof(a.fm[er], a.so[MN + er]);
+            Xf[2 * ((u >> 1) * MM + dpos<MM>(i)) + (u & 1)] = fmaf(a.rho, (w0 - w0n) + (w1 - w1r), a.hty[e]);
+        }
+        __syncthreads();
+        dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, al);
     } else {
         // kInit: the first iteration's v = H^T y, from HBM into the pairs at dpos order
         for (int idx = tid(); idx < T * MM / 2; idx += kNT) {
@@ -736,6 +785,77 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     }
 }
 
+// ---- the isotropic solve: one launch per iteration ------------------------------------------------------------
+// BT couples every plane through the per-pixel batch norm (ops.jl:6,10), so an iteration cannot finish inside one
+// workgroup.  As plane256_iso_kernel does at 256^2 (plane_iso.hip), each iteration k = 0 .. K-1 is one launch,
+// split at the norm:  B phase (k > 0; k = 0 starts from v = H^T y): v from s_k and f_k, line forward;
+// column phase (x C, ops.jl:86); line inverse -> x_{k+1}; A phase: s_{k+1} = D x_{k+1} + (s_k - f_k s_k) stored,
+// q per pixel (k = K - 1 writes x instead).  Between launches the 2-pass path's norm kernel (iso_r over the
+// planes' q, or the sharded sum / reducer / factor) forms f_{k+1}.  The spectrum never leaves the CU within a
+// launch; per pixel and iteration HBM moves s_k twice (B, A) and s_{k+1} once, H^T y and q: 32 B against the
+// 2-pass step's 44 and four launches.
+template <int MM, int NN>
+__global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restrict__ hty_all, const float* s_in,
+                                                           float* s_out, const float* __restrict__ fmap,
+                                                           float* __restrict__ q_all, float* __restrict__ x_all,
+                                                           const float* __restrict__ Ct, const float2* __restrict__ twM,
+                                                           const float2* __restrict__ twN, const float* __restrict__ prm,
+                                                           int k, int K) {
+    // s_in may equal s_out (in place, no trajectory): neither is __restrict__
+    using G = Geo<MM, NN>;
+    constexpr int NREG = G::NREG, NR = G::NR, NCC = G::NCC;
+    constexpr size_t MN = (size_t)MM * NN;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    float2* twm = reinterpret_cast<float2*>(smem_raw);
+    float2* twn = twm + MM;
+    for (int i = threadIdx.x; i < MM; i += kNT) twm[i] = twM[i];
+    for (int i = threadIdx.x; i < NN; i += kNT) twn[i] = twN[i];
+    const size_t plane = blockIdx.x;
+    const unsigned t = threadIdx.x;
+    Thr th;
+    th.buf = twn + NN;
+    th.twm = twm;
+    th.twn = twn;
+    th.kk = (int)(t / G::LS);
+    th.jt = (int)(t % G::LS);
+    th.act = t < (unsigned)(G::KBC * G::LS);
+    LineArgs la;
+    la.hty = hty_all + plane * MN;
+    la.xo = x_all + plane * MN;
+    la.tau = prm[0];
+    la.rho = prm[1];
+    la.so = s_in + plane * 2 * MN;
+    la.sn = s_out + plane * 2 * MN;
+    la.first = k == 0;
+    la.fm = fmap;
+    la.q = q_all + plane * MN;
+    float2 S[NREG];
+#pragma unroll
+    for (int r = 0; r < NREG; ++r) S[r] = make_float2(0.f, 0.f);
+    __syncthreads();
+    float2 hs[G::NLC * NCC];
+    if (k == 0) {
+        static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kInit>(S, hs, th, la); });
+    } else {
+        static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kIsoB>(S, hs, th, la); });
+    }
+    static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+    if (k == K - 1) {
+        static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
+        return;
+    }
+    // the A phase stages every chunk from S as it stands (no chunk's registers are rewritten in between), so the
+    // halo registers are S itself
+#pragma unroll
+    for (int c = 0; c < NCC; ++c) hs[c] = S[c * NR];
+    static_for<1, G::NLC>([&](auto ic) {
+        constexpr int C = decltype(ic)::value;
+#pragma unroll
+        for (int c = 0; c < NCC; ++c) hs[C * NCC + c] = S[c * NR + (C * G::TL - 2) / G::LS];
+    });
+    static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kIsoA>(S, hs, th, la); });
+}
+
 // ---- host side -----------------------------------------------------------------------------------------------
 // Shapes compiled here (M = line length, N = lines): square smooth sides the 2-pass path serves, and the small
 // power-of-two squares (the reference's 32 x 32 demo crops, src/ADMM_Deconv.jl:17-23; 64, 128)
@@ -752,6 +872,21 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 // squares until measured against their tuned 2-pass kernels.
 #define RS_SLOWER(X) X(128, 128) X(64, 64) X(32, 32)
 
+// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster
+#define RS_ISO_SLOWER(X) RS_SHAPES(X)
+
+bool has_iso_shape(int M, int N, bool all) {
+#define X(m, n) \
+    if (!all && M == m && N == n) return false;
+    RS_ISO_SLOWER(X)
+#undef X
+#define X(m, n) \
+    if (M == m && N == n) return true;
+    RS_SHAPES(X)
+#undef X
+    return false;
+}
+
 bool has_shape(int M, int N, bool all) {
 #define X(m, n) \
     if (!all && M == m && N == n) return false;
@@ -762,6 +897,23 @@ bool has_shape(int M, int N, bool all) {
     RS_SHAPES(X)
 #undef X
     return false;
+}
+
+int launch_iso(int M, int N, size_t planes, hipStream_t s, const float* hty, const float* s_in, float* s_out,
+               const float* fmap, float* q, float* x_out, const float* Ct, const float2* twM, const float2* twN,
+               const float* prm, int k, int K) {
+#define X(m, n)                                                                                                  \
+    if (M == m && N == n) {                                                                                      \
+        constexpr size_t lds = Geo<m, n>::lds_bytes();                                                           \
+        (void)hipFuncSetAttribute((const void*)resident_iso_kernel<m, n>,                                        \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+        resident_iso_kernel<m, n><<<dim3((unsigned)planes), kNT, lds, s>>>(hty, s_in, s_out, fmap, q, x_out, Ct, \
+                                                                            twM, twN, prm, k, K);                \
+        return 0;                                                                                                \
+    }
+    RS_SHAPES(X)
+#undef X
+    return -1;
 }
 
 int launch(int M, int N, size_t planes, hipStream_t s, const float* hty, float* sA, float* sB, float* traj,

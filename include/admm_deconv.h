@@ -269,7 +269,8 @@ enum {
     ADMM_PATH_SWEEP_2PASS = 10,       /* line_adj + column per step                                          */
     ADMM_PATH_SWEEP_2PASS_ISO = 11,   /* iso_adj_a / _r / _b + column per step                                */
     ADMM_PATH_SWEEP_RUNTIME = 12,     /* admm_generic_bwd.hip                                                 */
-    ADMM_PATH_SWEEP_RUNTIME_ISO = 13
+    ADMM_PATH_SWEEP_RUNTIME_ISO = 13,
+    ADMM_PATH_RESIDENT_ISO = 14       /* sides <= 256 isotropic: resident_iso_kernel + norm kernel per iteration */
 };
 int admm_query_paths(int M, int N, int iso, int kh, int mode, int flags, int want_hbar, int want_rho, int* fwd_path,
                      int* bwd_path);

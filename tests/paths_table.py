@@ -26,7 +26,14 @@ CASES = [
     ("128-forward-RESIDENT2", 128, 128, False, 15, F, 0, False, False, {"RESIDENT": 2}, "resident", None),
     ("demo32-record-RESIDENT2", 32, 32, False, 32, R, 0, False, False, {"RESIDENT": 2}, "resident", "sweep_2pass"),
     ("demo32-record-hbar-RESIDENT2", 32, 32, False, 32, R, HBAR, False, False, {"RESIDENT": 2}, "2pass", "sweep_2pass"),
-    ("64-iso-RESIDENT2", 64, 64, True, 0, F, 0, False, False, {"RESIDENT": 2}, "2pass_iso", None),
+    ("64-iso-RESIDENT2", 64, 64, True, 0, F, 0, False, False, {"RESIDENT": 2}, "resident_iso", None),
+    ("250-iso-RESIDENT2", 250, 250, True, 15, F, 0, False, False, {"RESIDENT": 2}, "resident_iso", None),
+    ("250-iso-record-RESIDENT2", 250, 250, True, 15, R, 0, False, False, {"RESIDENT": 2}, "resident_iso",
+     "sweep_runtime_iso"),
+    ("128-iso-backward-RESIDENT2", 128, 128, True, 0, B, 0, False, True, {"RESIDENT": 2}, "resident_iso",
+     "sweep_2pass_iso"),
+    ("128-iso-backward-hbar-RESIDENT2", 128, 128, True, 9, B, 0, True, True, {"RESIDENT": 2}, "2pass_iso",
+     "sweep_2pass_iso"),
     # c5 layers: ADMMDeconvF2 (lambda trainable, rho fixed) records mask bits / the lane-native iso trajectory
     ("c5-record-masks", 256, 256, False, 0, R, MASKS, False, False, {}, "fused", "sweep_fused"),
     ("c5-record-full", 256, 256, False, 0, R, 0, False, False, {}, "fused", "sweep_fused"),

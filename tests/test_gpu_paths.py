@@ -1,7 +1,7 @@
 """GPU: the kernels that actually launch for every combination of tests/paths_table.py are those of the path the
 library's decision table (admm_capi.hip plan_paths, queried by admm_query_paths) names.  Counted through the
 library profiler's kernel classes (include/admm_deconv.h ADMM_K_*), K = 4 iterations:
-  forward  fused / resident: one ADMM_K_PLANE launch; fused_iso: K (one per iteration); 2-pass, smooth and
+  forward  fused / resident: one ADMM_K_PLANE launch; fused_iso / resident_iso: K (one per iteration); 2-pass, smooth and
            runtime-length paths: none (column / line kernels instead);
   sweep    sweep_fused: one ADMM_K_ADJ launch; sweep_fused_iso: K and no column pass anywhere in the call;
            2-pass and runtime-length sweeps: >= K - 1 adjoint launches and column passes."""
@@ -50,7 +50,7 @@ def test_launched_kernels_follow_the_decision_table(dev, case):
             _lib.profile_enable(False)
     c = _counts()
     plane, adj, col = c.get("plane", 0), c.get("adjoint", 0), c.get("column", 0)
-    want_plane = {"fused": 1, "resident": 1, "fused_iso": K}.get(fwd, 0)
+    want_plane = {"fused": 1, "resident": 1, "fused_iso": K, "resident_iso": K}.get(fwd, 0)
     assert plane == want_plane, f"{cid}: forward path {fwd} but {plane} plane launches ({c})"
     if bwd == "sweep_fused":
         assert adj == 1, f"{cid}: {c}"
@@ -58,5 +58,5 @@ def test_launched_kernels_follow_the_decision_table(dev, case):
         assert adj == K and col == 0, f"{cid}: {c}"
     elif bwd is not None:
         assert adj >= K - 1 and col > 0, f"{cid}: {c}"
-    if fwd not in ("fused", "resident", "fused_iso"):
+    if fwd not in ("fused", "resident", "fused_iso", "resident_iso"):
         assert col >= K, f"{cid}: {c}"

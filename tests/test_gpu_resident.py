@@ -113,3 +113,77 @@ def test_resident_recorded_gradients_match_2pass(dev, side, res):
         d = np.linalg.norm((out[r][i] - out[0][i]).ravel()) / np.linalg.norm(out[0][i].ravel())
         assert d < 1e-5, f"{what}: resident recording vs 2-pass rel-L2 {d:.2e}"
     assert abs(out[r][2] - out[0][2]) <= 1e-4 * abs(out[0][2]), (out[r][2], out[0][2])
+
+
+# the isotropic solve (resident_iso_kernel: one launch per iteration, the norm kernel between), forced with
+# RESIDENT = 2, against the oracle and against the 2-pass isotropic kernels
+ISO_CASES = [
+    # (B, P, N, M, psf, lam, rho, K)
+    (3, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
+    (2, 3, 128, 128, None, 0.0041, 0.021, 20),                 # the c5 denoiser layer at 128 x 128
+    (4, 1, 96, 96, ("rand", 7, 5), 0.02, 0.1, 8),
+    (2, 3, 32, 32, ("rand", 32, 32), 0.00035, 0.3, 30),         # the reference demo shape, isotropic
+    (5, 1, 200, 200, ("gauss", 9, 1.5), 0.01, 0.05, 1),         # K = 1: the first launch is the last
+    (2, 1, 160, 160, ("gauss", 9, 1.5), 0.01, 0.05, 2),
+]
+
+
+def _solve_iso(dev, y, lam, rho, h, K, resident):
+    ht = None if h is None else torch.from_numpy(h).to(dev)
+    with _lib.option("RESIDENT", 2 * int(resident)):
+        x = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), lam, rho, ht, True, K)
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", ISO_CASES, ids=[f"iso-{c[0]}x{c[1]}x{c[2]}x{c[3]}-K{c[7]}" for c in ISO_CASES])
+def test_resident_iso_parity_vs_oracle_and_2pass(dev, case):
+    B, P, N, M, spec, lam, rho, K = case
+    rng = np.random.default_rng(N + 5 * M + K)
+    h = _psf(spec, rng)
+    y = synth.make_batch(B, M, N, h, P=P, g0=13)
+    with _lib.option("RESIDENT", 2):
+        assert _lib.query_paths(M, N, True, 0 if h is None else h.shape[1])[0] == "resident_iso"
+    got = _solve_iso(dev, y, lam, rho, h, K, True)
+    two = _solve_iso(dev, y, lam, rho, h, K, False)
+    ref = oracle_solve(y, lam, rho, h, True, K, "spectral", linear_only=K == 1, what="resident iso " + str(case))
+    assert_parity(got, ref, what="resident iso " + str(case))
+    d = np.linalg.norm((got - two).ravel()) / np.linalg.norm(two.ravel())
+    assert d < 1e-5, f"resident iso vs 2-pass rel-L2 {d:.2e}"
+
+
+def test_resident_iso_deterministic_and_couples_batch(dev):
+    """Bitwise deterministic (fixed-order norm over the planes); the batch norm couples the planes (ops.jl:6)."""
+    h = synth.gaussian_psf(9, 1.5)
+    y = torch.from_numpy(synth.make_batch(4, 120, 120, h)).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    with _lib.option("RESIDENT", 2):
+        a = admm_deconv.tvd_fft(y, 0.01, 0.05, ht, True, 7)
+        b = admm_deconv.tvd_fft(y, 0.01, 0.05, ht, True, 7)
+        one = admm_deconv.tvd_fft(y[:1].contiguous(), 0.01, 0.05, ht, True, 7)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert not torch.allclose(a[:1], one, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("side", [250, 128])
+def test_resident_iso_recorded_gradients_match_2pass(dev, side):
+    """Isotropic training step at a resident shape: the recording forward (s_k and |s_k| in the natural layout)
+    feeds the 2-pass / runtime-length isotropic sweep; gradients against the all-2-pass recording."""
+    h = synth.gaussian_psf(9, 1.5)
+    yb = synth.make_batch(2, side, side, h, P=2, g0=3)
+    out = {}
+    for res in (2, 0):
+        with _lib.option("RESIDENT", res):
+            y = torch.from_numpy(yb).to(dev).requires_grad_(True)
+            lam = torch.tensor([0.0041], device=dev, requires_grad=True)
+            rho = torch.tensor([0.021], device=dev, requires_grad=True)
+            x = admm_deconv.tvd_fft(y, lam, rho, torch.from_numpy(h).to(dev), True, 6)
+            (x * x).sum().backward()
+            torch.cuda.synchronize()
+            out[res] = (x.detach().cpu().numpy(), y.grad.cpu().numpy(), float(lam.grad), float(rho.grad))
+    for i, what in ((0, "x"), (1, "y_bar")):
+        d = np.linalg.norm((out[2][i] - out[0][i]).ravel()) / np.linalg.norm(out[0][i].ravel())
+        assert d < 1e-5, f"{what}: resident iso recording vs 2-pass rel-L2 {d:.2e}"
+    for i in (2, 3):
+        assert abs(out[2][i] - out[0][i]) <= 1e-4 * abs(out[0][i]), (i, out[2][i], out[0][i])

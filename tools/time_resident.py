@@ -22,6 +22,9 @@ for _a in [a for a in sys.argv[1:] if "=" in a]:
 TIME_ONLY = "--time-only" in sys.argv
 if TIME_ONLY:
     sys.argv.remove("--time-only")
+ISO = "--iso" in sys.argv          # the isotropic solve (resident_iso_kernel vs the 2-pass isotropic kernels)
+if ISO:
+    sys.argv.remove("--iso")
 SHAPES = [(250, 250, 256, 25)]
 if len(sys.argv) > 1:
     SHAPES = [tuple(int(v) for v in (a.split(",") + ["25"])[:4]) for a in sys.argv[1:]]
@@ -29,7 +32,7 @@ if len(sys.argv) > 1:
 
 def solve(y, h, K, resident):
     with _lib.option("RESIDENT", 2 * int(resident)):   # 2: every compiled shape
-        x = admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K)
+        x = admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, ISO, K)
     torch.cuda.synchronize()
     return x
 
@@ -56,7 +59,7 @@ def main():
             b = solve(y, hh, k_chk, False)
             ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(yb.astype(np.float64)),
                                                             np.float32(synth.LAMBDA), np.float32(synth.RHO),
-                                                            oracle_np.psf_from_c(hp if with_h else None), False, k_chk))
+                                                            oracle_np.psf_from_c(hp if with_h else None), ISO, k_chk))
             r = {"shape": [N, M], "K": k_chk, "psf": with_h, "resident_vs_2pass": rel(a, b.cpu().numpy()),
                  "resident_vs_oracle": rel(a, ref), "2pass_vs_oracle": rel(b, ref),
                  "finite": bool(torch.isfinite(a).all())}
@@ -71,7 +74,7 @@ def main():
             t0 = time.perf_counter()
             with _lib.option("RESIDENT", 2 * int(res)):
                 for _ in range(reps):
-                    admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K)
+                    admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, ISO, K)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / reps
             _lib.profile_reset()
@@ -83,7 +86,7 @@ def main():
                 ms, n = _lib.profile_get(cls)
                 if n:
                     ks[name] = [round(ms, 4), n]
-            r = {"shape": [N, M], "batch": B, "K": K, "resident": res, "ms": round(1000 * dt, 3),
+            r = {"shape": [N, M], "batch": B, "K": K, "iso": ISO, "resident": res, "ms": round(1000 * dt, 3),
                  "img_s": round(B / dt, 1), "kernel_ms_launches": ks}
             print(json.dumps(r), flush=True)
             out.append(r)
