@@ -29,8 +29,10 @@ def _inputs(M):
     return h, y, xbar
 
 
-def _worker(rank, world, port, q, M, need_rho):
+def _worker(rank, world, port, q, M, need_rho, resident=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from admm_deconv import _lib
+    _lib.set_option("RESIDENT", resident if resident else 1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     h, y, xbar = _inputs(M)
@@ -62,9 +64,23 @@ def _rel(a, b):
     return float(np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b))
 
 
-@pytest.mark.parametrize("M,need_rho", [(64, True), (256, True), (256, False)],
-                         ids=["2pass", "fused-fwd", "fused-fwd+sweep"])
-def test_iso_sharded_two_processes(dev, M, need_rho):
+@pytest.mark.parametrize("M,need_rho,resident", [(64, True, 0), (256, True, 0), (256, False, 0), (120, False, 2)],
+                         ids=["2pass", "fused-fwd", "fused-fwd+sweep", "resident-iso"])
+def test_iso_sharded_two_processes(dev, M, need_rho, resident):
+    """resident-iso: 120 x 120 with ADMM_OPT_RESIDENT = 2, the isotropic CU-resident solve (resident_iso_kernel),
+    whose norm kernel splits into the shard sum, the reducer and the factor the same way."""
+    from admm_deconv import _lib
+    _lib.set_option("RESIDENT", resident if resident else 1)
+    try:
+        _iso_sharded(dev, M, need_rho, resident)
+    finally:
+        _lib.set_option("RESIDENT", 1)
+
+
+def _iso_sharded(dev, M, need_rho, resident):
+    if resident:
+        from admm_deconv import _lib
+        assert _lib.query_paths(M, M, True, 7)[0] == "resident_iso"
     h, y, xbar = _inputs(M)
     ht = torch.from_numpy(h).to(dev)
     x0 = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), LAM, RHO, ht, True, K).cpu().numpy()
@@ -75,7 +91,7 @@ def test_iso_sharded_two_processes(dev, M, need_rho):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, M, need_rho)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, M, need_rho, resident)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
