@@ -745,6 +745,8 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     la.so = nullptr;
     la.sn = nullptr;
     la.first = true;
+    la.fm = nullptr;   // isotropic modes only
+    la.q = nullptr;
     float2 S[NREG];
 #pragma unroll
     for (int r = 0; r < NREG; ++r) S[r] = make_float2(0.f, 0.f);
