@@ -1256,7 +1256,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
         rc = ln.run(ADMM_K_ADJ, [&] {
             return pk::launch_plane_adj(x_bar, ws + bl.f.F, tr.m ? static_cast<const void*>(tr.m) : tr.s, dxK,
                                        reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s,
-                                       nullptr, tr.m != nullptr);
+                                       nullptr, tr.m != nullptr, opt(ADMM_OPT_PLANE_STAGGER));
         });
         if (rc) return rc;
         red_rows = (int)planes;
@@ -1755,7 +1755,7 @@ int backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, float* r
     rc = ln.run(ADMM_K_ADJ, [&] {
         return admm::plane::launch_plane_adj(x_bar, ws + L.F, ws + L.traj, dxK, reinterpret_cast<float4*>(ws + L.sbar),
                                              reinterpret_cast<float2*>(ws + L.vsl), vbuf, part,
-                                             prm, K, planes, s, &br, masks);
+                                             prm, K, planes, s, &br, masks, opt(ADMM_OPT_PLANE_STAGGER));
     });
     if (rc) return rc;
     double* rt = reinterpret_cast<double*>(ws + L.rt);

@@ -58,7 +58,7 @@ hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream
 // chcat layout; vout and part per grid plane).
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s, const Branches* br = nullptr, bool masks = false);
+                            hipStream_t s, const Branches* br = nullptr, bool masks = false, int stagger = 0);
 
 // Isotropic (BT) solve at 256 x 256 (plane_iso.hip): iteration k = 0 .. K-1 of every plane (hln: H^T y,
 // lane-native, written at k = 0; s_in / s_out: s_k / s_{k+1}, the same state buffer, or trajectory slots k-1 / k

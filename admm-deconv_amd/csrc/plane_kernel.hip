@@ -944,7 +944,13 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
                                                            const float4* __restrict__ dxK, float4* __restrict__ sbar,
                                                            float2* __restrict__ vsl, float* __restrict__ vout,
                                                            double* __restrict__ part, const float* __restrict__ prm, int K,
-                                                           Branches br) {
+                                                           Branches br, int stagger_ticks) {
+    // Phase stagger (experiment option ADMM_OPT_PLANE_STAGGER): odd workgroups of the first wave start
+    // `stagger_ticks` of the 100 MHz realtime clock late, so that two CU groups' row phases alternate.
+    if (stagger_ticks > 0 && (blockIdx.x & 1) && blockIdx.x < 256) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger_ticks) __builtin_amdgcn_s_sleep(10);
+    }
     const BranchOf bo = branch_of(br, blockIdx.x);
     Cf += (size_t)bo.i * br.tab_f;
     C0b += (size_t)bo.i * br.tab_f;

@@ -69,7 +69,7 @@ hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream
 
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s, const Branches* brp, bool masks) {
+                            hipStream_t s, const Branches* brp, bool masks, int stagger) {
     const Tables t = carve(tables);
     const Branches br = brp ? *brp : one_branch();
     if (masks && dxK) return hipErrorInvalidValue;   // rho_bar needs the full trajectory
@@ -79,7 +79,7 @@ hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* t
         (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<MK, WV>,                                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);                \
         hipLaunchKernelGGL((plane256_adj_kernel<MK, WV>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s,    \
-                           xbar, t.Cf, t.C0b, traj, slot, dxK, sbar, vsl, vout, part, prm, K, br);           \
+                           xbar, t.Cf, t.C0b, traj, slot, dxK, sbar, vsl, vout, part, prm, K, br, stagger);         \
     }
     X(false, false) X(false, true) X(true, false) X(true, true)
 #undef X

@@ -122,7 +122,9 @@ ISO_CASES = [
     (3, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
     (2, 3, 128, 128, None, 0.0041, 0.021, 20),                 # the c5 denoiser layer at 128 x 128
     (4, 1, 96, 96, ("rand", 7, 5), 0.02, 0.1, 8),
-    (2, 3, 32, 32, ("rand", 32, 32), 0.00035, 0.3, 30),         # the reference demo shape, isotropic
+    # the reference demo shape, isotropic: lambda 0.0008 puts the BT prox live in 21 % of the pairs while an
+    # fp32 evaluation stays 1.6e-6 off the oracle (0.00035: 99.97 % live, but fp32 itself is 4.7e-5 off)
+    (2, 3, 32, 32, ("rand", 32, 32), 0.0008, 0.3, 30),
     (5, 1, 200, 200, ("gauss", 9, 1.5), 0.01, 0.05, 1),         # K = 1: the first launch is the last
     (2, 1, 160, 160, ("gauss", 9, 1.5), 0.01, 0.05, 2),
 ]
