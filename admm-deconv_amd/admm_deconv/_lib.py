@@ -19,10 +19,11 @@ ADMM_E_HIP = -4
 ADMM_E_REDUCER = -5
 
 # library options (admm_set_option, include/admm_deconv.h)
-OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER, OPT_SMOOTH, OPT_RESIDENT = range(9)
+OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER, OPT_SMOOTH, OPT_RESIDENT, \
+    OPT_MIN_PLANES = range(10)
 OPTIONS = {"FUSED": OPT_FUSED, "FUSED_ADJ": OPT_FUSED_ADJ, "LINE_T": OPT_LINE_T, "COL_THREADS": OPT_COL_THREADS,
            "GEN_TM": OPT_GEN_TM, "GEN_KN": OPT_GEN_KN, "PLANE_STAGGER": OPT_PLANE_STAGGER,
-           "SMOOTH": OPT_SMOOTH, "RESIDENT": OPT_RESIDENT}
+           "SMOOTH": OPT_SMOOTH, "RESIDENT": OPT_RESIDENT, "MIN_PLANES": OPT_MIN_PLANES}
 
 K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE, K_ADJ = range(8)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
@@ -150,7 +151,7 @@ def load():
     L.admm_copy_async.restype = c_int
     L.admm_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
     L.admm_query_paths.restype = c_int
-    L.admm_query_paths.argtypes = [c_int] * 8 + [ctypes.POINTER(c_int)] * 2
+    L.admm_query_paths.argtypes = [c_int] * 4 + [ctypes.c_longlong] + [c_int] * 4 + [ctypes.POINTER(c_int)] * 2
     L.admm_path_name.restype = ctypes.c_char_p
     L.admm_path_name.argtypes = [c_int]
     _lib = L
@@ -187,12 +188,13 @@ def multi_workspace_bytes(M, N, P, B, nbranch, maxit, flags):
 MODE_FORWARD, MODE_RECORD, MODE_BACKWARD = 0, 1, 2
 
 
-def query_paths(M, N, iso=False, kh=0, mode=MODE_FORWARD, flags=0, want_hbar=False, want_rho=False):
-    """admm_query_paths: (forward path name, reverse-sweep path name or None) the library would run."""
+def query_paths(M, N, iso=False, kh=0, mode=MODE_FORWARD, flags=0, want_hbar=False, want_rho=False, planes=0):
+    """admm_query_paths: (forward path name, reverse-sweep path name or None) the library would run for a call
+    of `planes` = P * B planes (0: no plane-count rule, OPT_MIN_PLANES)."""
     L = load()
     f, b = ctypes.c_int(0), ctypes.c_int(0)
-    check(L.admm_query_paths(M, N, int(iso), kh, mode, flags, int(want_hbar), int(want_rho), ctypes.byref(f),
-                             ctypes.byref(b)))
+    check(L.admm_query_paths(M, N, int(iso), kh, int(planes), mode, flags, int(want_hbar), int(want_rho),
+                             ctypes.byref(f), ctypes.byref(b)))
     return L.admm_path_name(f.value).decode(), (L.admm_path_name(b.value).decode() if b.value else None)
 
 

@@ -63,7 +63,7 @@ constexpr int kGenMax = 4096;
 // Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
 // choices; the others exist for tests (fused vs 2-pass) and tuning experiments.  A recording stores
 // the option values it was made with, and its replay rejects a change (RecTag below).
-std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}};
+std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {-1}};
 int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 
 // ADMM_OPT_FUSED = 0 forces the 2-pass path (tests compare the two).
@@ -366,7 +366,31 @@ struct PathIn {
     int mode;            // ADMM_MODE_FORWARD, ADMM_MODE_RECORD, ADMM_MODE_BACKWARD
     int rec_flags;       // ADMM_REC_* (record)
     bool h_bar, rho_bar; // backward: gradients asked for
+    size_t planes;       // P * B of the call (0: unknown, no plane-count rule)
 };
+// Plane counts from which the one-workgroup-per-plane paths beat the 2-pass kernels (ADMM_OPT_MIN_PLANES = -1).
+// A per-plane grid uses one CU per plane for the whole solve, so below about one CU wave it leaves CUs idle
+// while the 2-pass kernels spread every plane over many workgroups.  Measured on MI355X (tools/time_small.py,
+// profiles/r04_small_batch_paths.jsonl; K = 25 forward, K = 50 recording + sweep):
+//   fused 256^2 anisotropic  forward 96 planes 1.32 vs 1.34 ms, 64: 1.29 vs 1.07; recording + sweep 96: 5.55 vs
+//                            6.24, 64: 5.34 vs 4.75  -> 96
+//   fused_iso 256^2          128: 2.03 vs 2.13, 64: 1.84 vs 1.40  -> 112
+//   resident 250^2           192: 2.53 vs 2.96, 128: 2.48 vs 1.99; 128^2 256: 0.88 vs 0.93, 128: 0.84 vs 0.62
+//                            -> 192 for sides >= 128 (smaller sides: every batch, the per-plane latency is small)
+//   resident_iso             96^2 x 256 0.93 vs 1.17, 32^2 x 512 0.57 vs 0.69; 128^2 x 192 1.45 vs 0.99 -> 256
+enum MinPlanesFor { kMinFused, kMinFusedIso, kMinResident, kMinResidentIso };
+bool enough_planes(const PathIn& q, MinPlanesFor which) {
+    const int o = opt(ADMM_OPT_MIN_PLANES);
+    if (q.planes == 0 || o == 0) return true;
+    if (o > 0) return q.planes >= (size_t)o;
+    switch (which) {
+        case kMinFused: return q.planes >= 96;
+        case kMinFusedIso: return q.planes >= 112;
+        case kMinResident: return std::max(q.M, q.N) < 128 || q.planes >= 192;
+        case kMinResidentIso: return q.planes >= 256;
+    }
+    return true;
+}
 struct PathPlan {
     bool want_h = false;     // the forward records the dim-2 spectra h_bar needs (2-pass column pass)
     bool ln_traj = false;    // the fused 256^2 forward records s lane-native
@@ -396,13 +420,13 @@ const FwdRule kFwdRules[] = {
     {ADMM_PATH_RESIDENT, [](const PathIn& q, const TrajFlags& t) {
          return !q.iso && !t.v && !t.nrm && !t.m && opt(ADMM_OPT_RESIDENT) != 0 &&
                 (!generic_shape(q.M, q.N) || opt(ADMM_OPT_SMOOTH) != 0) &&
-                admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
+                admm::rs::has_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2) && enough_planes(q, kMinResident);
      }},
     // isotropic: the split-iteration CU-resident solve (resident_iso_kernel, one launch per iteration with the
     // norm kernel between); it records s_k and |s_k| in the natural layout the 2-pass / runtime sweeps read
     {ADMM_PATH_RESIDENT_ISO, [](const PathIn& q, const TrajFlags& t) {
          return q.iso && !t.v && opt(ADMM_OPT_RESIDENT) != 0 && (!generic_shape(q.M, q.N) || opt(ADMM_OPT_SMOOTH) != 0) &&
-                admm::rs::has_iso_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2);
+                admm::rs::has_iso_shape(q.M, q.N, opt(ADMM_OPT_RESIDENT) >= 2) && enough_planes(q, kMinResidentIso);
      }},
     // compile-time-plan kernels when this build has either length (admm_smooth.hip), else runtime plans
     {ADMM_PATH_SMOOTH, [](const PathIn& q, const TrajFlags&) {
@@ -412,12 +436,13 @@ const FwdRule kFwdRules[] = {
     {ADMM_PATH_RUNTIME, [](const PathIn& q, const TrajFlags&) { return generic_shape(q.M, q.N); }},
     // 256 x 256 anisotropic: one workgroup per plane runs all K iterations (plane_kernel.hip)
     {ADMM_PATH_FUSED, [](const PathIn& q, const TrajFlags& t) {
-         return fused_shape(q.M, q.N, q.iso) && !t.v && fused_enabled();
+         return fused_shape(q.M, q.N, q.iso) && !t.v && fused_enabled() && enough_planes(q, kMinFused);
      }},
     // 256 x 256 isotropic: split-iteration per-plane kernels (plane_iso.hip); a recording only in its own
     // lane-native layout (the fused sweep's)
     {ADMM_PATH_FUSED_ISO, [](const PathIn& q, const TrajFlags& t) {
-         return q.iso && fused_tables_shape(q.M, q.N) && (!t.s || t.iso_lane) && !t.v && fused_enabled();
+         return q.iso && fused_tables_shape(q.M, q.N) && (!t.s || t.iso_lane) && !t.v && fused_enabled() &&
+                enough_planes(q, kMinFusedIso);
      }},
     {ADMM_PATH_2PASS_ISO, [](const PathIn& q, const TrajFlags&) { return q.iso; }},
     {ADMM_PATH_2PASS, [](const PathIn&, const TrajFlags&) { return true; }},
@@ -429,11 +454,12 @@ PathPlan plan_paths(const PathIn& q) {
     if (rec) {
         pl.want_h = (q.mode == ADMM_MODE_RECORD ? (q.rec_flags & ADMM_REC_HBAR) != 0 : q.h_bar) && q.psf;
         // the fused kernel records s in its lane-native layout (no dim-2 spectra: not with h_bar)
-        pl.ln_traj = fused_shape(q.M, q.N, q.iso) && fused_enabled() && !pl.want_h;
+        pl.ln_traj = fused_shape(q.M, q.N, q.iso) && fused_enabled() && !pl.want_h && enough_planes(q, kMinFused);
         // mask-bit trajectory (fused forward + fused reverse sweep): asked for by a recording (ADMM_REC_MASKS),
         // taken by the combined call whenever rho_bar is not wanted; isotropic at 256 x 256 the same flag
         // selects the split-iteration trajectory (s and |s| lane-native) for the fused isotropic sweep
-        const bool iso_ok = q.iso && fused_tables_shape(q.M, q.N) && !pl.want_h && fused_enabled() && fused_adj_enabled();
+        const bool iso_ok = q.iso && fused_tables_shape(q.M, q.N) && !pl.want_h && fused_enabled() && fused_adj_enabled() &&
+                            enough_planes(q, kMinFusedIso);
         const bool masks_ok = (pl.ln_traj && !q.iso && fused_adj_enabled()) || iso_ok;
         pl.masks = masks_ok && (q.mode == ADMM_MODE_RECORD ? (q.rec_flags & ADMM_REC_MASKS) != 0 : !q.rho_bar);
         pl.iso_lane = pl.masks && q.iso;
@@ -1114,7 +1140,7 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rec_forget(workspace);   // whatever was recorded there is overwritten now
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
     const size_t MN = (size_t)M * N;
-    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false});
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false, planes});
     for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
         rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
                          maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red, pl.fwd);
@@ -1150,7 +1176,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
         pflags = (h_bar != nullptr ? ADMM_REC_HBAR : 0) | (it != g_rec.end() && it->second.masks ? ADMM_REC_MASKS : 0);
     }
     const PathPlan plan = plan_paths({M, N, iso != 0, kh > 0, phases == 3 ? ADMM_MODE_BACKWARD : ADMM_MODE_RECORD, pflags,
-                                  h_bar != nullptr, rho_bar != nullptr});
+                                  h_bar != nullptr, rho_bar != nullptr, planes});
     const bool want_h = plan.want_h;
     const bool ln_traj = plan.ln_traj;
     const bool use_masks = plan.masks;
@@ -1815,7 +1841,7 @@ int admm_tvd_backward_workspace_bytes(int M, int N, int P, int B, int kh, int kw
     if (rc) return rc;
     if (maxit < 0) return fail(ADMM_E_INVALID, "maxit must be >= 0");
     if ((size_t)P * B > 65535) return fail(ADMM_E_UNSUPPORTED, "the adjoint takes at most 65535 planes per call (split the batch)");
-    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_RECORD, want_hbar, false, false});
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_RECORD, want_hbar, false, false, (size_t)P * B});
     *out_bytes = make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, pl.want_h, iso != 0, pl.masks && !iso).total;
     return ADMM_OK;
 }
@@ -1926,14 +1952,15 @@ int admm_profile_get(int kernel_class, double* total_ms, long long* launches) {
     return ADMM_OK;
 }
 
-int admm_query_paths(int M, int N, int iso, int kh, int mode, int flags, int want_hbar, int want_rho, int* fwd_path,
-                     int* bwd_path) {
+int admm_query_paths(int M, int N, int iso, int kh, long long planes, int mode, int flags, int want_hbar, int want_rho,
+                     int* fwd_path, int* bwd_path) {
     if (!fwd_path || !bwd_path) return fail(ADMM_E_INVALID, "admm_query_paths: NULL output");
     if (mode != ADMM_MODE_FORWARD && mode != ADMM_MODE_RECORD && mode != ADMM_MODE_BACKWARD)
         return fail(ADMM_E_INVALID, "admm_query_paths: unknown mode %d", mode);
     const int rc = check_shape(M, N, 1, 1, kh, kh, iso);
     if (rc) return rc;
-    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, mode, flags, want_hbar != 0, want_rho != 0});
+    if (planes < 0) return fail(ADMM_E_INVALID, "admm_query_paths: planes must be >= 0");
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, mode, flags, want_hbar != 0, want_rho != 0, (size_t)planes});
     *fwd_path = pl.fwd;
     *bwd_path = pl.bwd;
     return ADMM_OK;

@@ -269,16 +269,39 @@ struct Geo {
             if (fits(n) && n * nr(n) <= min_regs() + 2) return n;
         return 0;
     }
-#ifdef RS_NCC_FORCE   // experiments: column chunk count forced
-    static constexpr int NCC = fits(RS_NCC_FORCE) ? RS_NCC_FORCE : ncc();
-#else
-    static constexpr int NCC = ncc();              // column chunks
+    // Register-column layout (RS_RCOL, column_chunk_rc): LS line slots with LS | NN, so that a thread's lines
+    // jt, jt + LS, .. are one decimated column of L2 = NN / LS points: an L2-point DFT in registers, a twiddle,
+    // and LS-point DFTs across the LS threads of a bin (one LDS exchange each way).  LS even (line pairs), at
+    // most 16 and at most L2 (every thread gets a k1 of the cross-thread stage); fewest registers, then
+    // fewest chunks.  0: no such LS (the shape keeps the LDS-pass column phase).
+    static constexpr bool rc_ok(int l) {
+        return l >= 2 && l % 2 == 0 && NN % l == 0 && l <= 16 && l * l <= NN && NN / l <= 32 &&
+               sm::max_prime(NN / l) <= 31 && (kNT / l) * (NN | 1) <= kBudget;
+    }
+    static constexpr int rc_regs(int l) { return cdiv(H, kNT / l) * (NN / l); }
+    static constexpr int rc_ls() {
+        int best = 0;
+        for (int l = 2; l <= 16; l += 2)
+            if (rc_ok(l) && (best == 0 || rc_regs(l) < rc_regs(best) ||
+                             (rc_regs(l) == rc_regs(best) && cdiv(H, kNT / l) < cdiv(H, kNT / best))))
+                best = l;
+        return best;
+    }
+#ifndef RS_RCOL
+#define RS_RCOL 0
 #endif
-    static constexpr int KBC = kbc(NCC);           // bins per column chunk
-    static constexpr int LS = ls(NCC);             // line slots
-    static constexpr int NR = nr(NCC);             // registers per column chunk
+    static constexpr int RCLS = RS_RCOL ? rc_ls() : 0;
+    static constexpr bool RC = RCLS != 0;          // register-column phase
+#ifdef RS_NCC_FORCE   // experiments: column chunk count forced
+    static constexpr int NCC = RC ? cdiv(H, kNT / RCLS) : fits(RS_NCC_FORCE) ? RS_NCC_FORCE : ncc();
+#else
+    static constexpr int NCC = RC ? cdiv(H, kNT / RCLS) : ncc();   // column chunks
+#endif
+    static constexpr int KBC = RC ? kNT / RCLS : kbc(NCC);         // bins per column chunk
+    static constexpr int LS = RC ? RCLS : ls(NCC);                 // line slots
+    static constexpr int NR = RC ? NN / RCLS : nr(NCC);            // registers per column chunk
     static constexpr int NREG = NCC * NR;          // spectrum registers (float2) per thread
-    static constexpr int FS = fs(NCC);
+    static constexpr int FS = RC ? (NN | 1) : fs(NCC);
     static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
     // line chunks: TL lines (a multiple of LS: whole registers) + a halo pair either side, as complex pairs
     static constexpr int tl(int n) { return cdiv(cdiv(NN, n), LS) * LS; }
@@ -377,6 +400,86 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, 
         for (int r = 0; r < NR; ++r) S[R0 + r] = col[r * G::LS + th.jt];
     }
     __syncthreads();
+}
+
+// ---- register column phase, chunk C (Geo::RC): the dim-2 transform of bin kc0 + kk split as NN = LS x L2 --------
+// Thread (kk, jt) holds x[jt + LS r], r < L2, of its bin (registers [C NR, C NR + NR)).  With j = jt + LS r and
+// k = k1 + L2 k2:  X[k] = sum_jt W_LS^{jt k2} W_NN^{jt k1} (sum_r x[jt + LS r] W_L2^{r k1}).
+//   1. L2-point DFT over the thread's registers, x W_NN^{jt k1} (jt k1 < NN: one table entry, no reduction);
+//   2. to LDS at slot k1 LS + jt of the bin's column; barrier;
+//   3. thread jt takes k1 = jt, jt + LS, ..: LS-point DFT over jt -> X[k1 + L2 k2], x Ct at that frequency (the
+//      C / (MN) of ops.jl:86), inverse LS-point DFT, in place; barrier;
+//   4. slot k1 LS + jt back, x conj W_NN^{jt k1}, inverse L2-point DFT -> the registers.
+// Unnormalised both ways, as the LDS-pass phase: the same arithmetic contract, two LDS round trips and three
+// barriers per chunk instead of a round trip and a barrier per radix pass.
+template <int MM, int NN, int C, int NREG>
+__device__ __forceinline__ void column_chunk_rc(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
+    using G = Geo<MM, NN>;
+    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
+    constexpr int LS = G::LS, L2 = NN / LS, NR = G::NR, R0 = C * NR, KB = G::KBC, H = G::H, FB = G::FS;
+    static_assert(NR == L2 && LS * L2 == NN, "register column layout");
+    constexpr int kc0 = C * KB, kc1 = imin(H, kc0 + KB), kc = kc1 - kc0;
+    constexpr int NK = cdiv(L2, LS);   // k1 values per thread in step 3
+    const int kk = th.kk, jt = th.jt;
+    const bool live = kk < kc;         // the thread's bin is in this chunk
+    float2 v[L2];
+#pragma unroll
+    for (int r = 0; r < L2; ++r) v[r] = S[R0 + r];
+    dftR<L2, false>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < L2; ++k1) v[k1] = cmul(v[k1], twv<false>(th.twn, jt * k1));
+    // multipliers of step 3, issued before the exchange (one L2 latency per chunk): bin kc0 + kk, frequency
+    // k1 + L2 k2 at Ct[(k1 + L2 k2) H + bin]; the k2 row is a constant SGPR offset
+    const rsrc_t rc = make_rsrc(Ct, (unsigned)(H * NN * 4));
+    float cm[NK][LS];
+#pragma unroll
+    for (int m = 0; m < NK; ++m) {
+        const int k1 = imin(jt + LS * m, L2 - 1);
+        const unsigned vo = 4u * (unsigned)(k1 * H + kc0 + (live ? kk : 0));
+#pragma unroll
+        for (int k2 = 0; k2 < LS; ++k2) cm[m][k2] = bld1(rc, vo, 4u * (unsigned)(k2 * L2 * H));
+    }
+    float2* col = th.buf + kk * FB;
+    if (live) {
+#pragma unroll
+        for (int k1 = 0; k1 < L2; ++k1) col[k1 * LS + jt] = v[k1];
+    }
+    __syncthreads();
+    if (live) {
+#pragma unroll
+        for (int m = 0; m < NK; ++m) {
+            const int k1 = jt + LS * m;
+            if (m < NK - 1 || k1 < L2) {
+                float2 w[LS];
+#pragma unroll
+                for (int j = 0; j < LS; ++j) w[j] = col[k1 * LS + j];
+                dftR<LS, false>(w);
+#pragma unroll
+                for (int k2 = 0; k2 < LS; ++k2) w[k2] = cscale(w[k2], cm[m][k2]);
+                dftR<LS, true>(w);
+#pragma unroll
+                for (int j = 0; j < LS; ++j) col[k1 * LS + j] = w[j];
+            }
+        }
+    }
+    __syncthreads();
+    {   // every thread reads back every register (threads past the chunk's bins: a valid column, never used)
+        const float2* cr = th.buf + imin(kk, kc - 1) * FB;
+#pragma unroll
+        for (int k1 = 0; k1 < L2; ++k1) v[k1] = cr[k1 * LS + jt];
+    }
+#pragma unroll
+    for (int k1 = 1; k1 < L2; ++k1) v[k1] = cmul(v[k1], twv<true>(th.twn, jt * k1));
+    dftR<L2, true>(v);
+#pragma unroll
+    for (int r = 0; r < L2; ++r) S[R0 + r] = v[r];
+    __syncthreads();
+}
+
+template <int MM, int NN, int C, int NREG>
+__device__ __forceinline__ void column_phase_chunk(float2 (&S)[NREG], const Thr& th, const float* __restrict__ Ct) {
+    if constexpr (Geo<MM, NN>::RC) column_chunk_rc<MM, NN, C>(S, th, Ct);
+    else column_chunk<MM, NN, C>(S, th, Ct);
 }
 
 // ---- line phase, chunk C: lines [jc0, jc1) ---------------------------------------------------------------
@@ -756,7 +859,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #pragma unroll 1
     for (int it = 1; it <= maxit; ++it) {
 #ifndef RS_SKIP_COL
-        static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+        static_for<0, G::NCC>([&](auto ic) { column_phase_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
 #endif
         if (it == maxit) {
             static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
@@ -841,7 +944,7 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
     } else {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kIsoB>(S, hs, th, la); });
     }
-    static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+    static_for<0, G::NCC>([&](auto ic) { column_phase_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
     if (k == K - 1) {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
         return;
@@ -868,14 +971,18 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
 #define RS_SHAPES(X) RS_SHAPES_OVERRIDE(X)
 #endif
 
-// Compiled shapes where the 2-pass smooth kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the
-// 2-pass path; 2 forces the resident kernel on every compiled shape).  No smooth shape since the spills went
-// (round 4: 240^2 resident 77.8k img/s vs 74.2k 2-pass, profiles/r04_resident_shapes.jsonl); the power-of-two
-// squares until measured against their tuned 2-pass kernels.
-#define RS_SLOWER(X) X(128, 128) X(64, 64) X(32, 32)
+// Compiled shapes where the 2-pass kernels measured faster (ADMM_OPT_RESIDENT = 1 leaves them to the 2-pass
+// path; 2 forces the resident kernel on every compiled shape).  None: no smooth shape since the spills went
+// (round 4: 240^2 resident 77.8k img/s vs 74.2k 2-pass, profiles/r04_resident_shapes.jsonl), and the power-of-two
+// squares beat their tuned 2-pass kernels too (128^2 x 256 0.91 vs 0.94 ms, 64^2 x 1024 0.68 vs 0.94, 32^2 x 2048
+// 0.61 vs 1.59; profiles/r04_resident_pow2.jsonl).  Small batches are left to the 2-pass kernels by plan_paths.
+#define RS_SLOWER(X)
 
-// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster
-#define RS_ISO_SLOWER(X) RS_SHAPES(X)
+// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster, or that are not
+// measured yet (profiles/r04_resident_iso.jsonl: 96^2 x 256 0.93 vs 1.17 ms and 32^2 x 512 0.57 vs 0.69 resident;
+// 128^2 x 192 1.45 vs 0.99 and 250^2 x 64 4.41 vs 1.84 2-pass -- one launch per iteration with one plane per CU
+// needs a full wave of planes)
+#define RS_ISO_SLOWER(X) X(250, 250) X(240, 240) X(200, 200) X(192, 192) X(160, 160) X(128, 128) X(120, 120) X(64, 64)
 
 bool has_iso_shape(int M, int N, bool all) {
 #define X(m, n) \

@@ -243,7 +243,13 @@ enum {
                                     non-power-of-two shapes admm_resident.hip compiled and measured faster
                                     (anisotropic, no h_bar trajectory); 2: every compiled shape; 0: the
                                     2-pass smooth kernels                                                     */
-    ADMM_OPT_COUNT = 9
+    ADMM_OPT_MIN_PLANES = 9,     /* -1 (default): the one-workgroup-per-plane paths (fused, fused_iso, resident,
+                                    resident_iso) are taken only from the measured plane counts where they beat
+                                    the multi-workgroup 2-pass kernels (admm_capi.hip kMinPlanes; a smaller batch
+                                    runs the 2-pass kernels, so a plane's result can differ by fp32 rounding
+                                    between batch sizes); 0: those paths at every batch size (results independent
+                                    of the batch size, as for anisotropic solves before); n > 0: from n planes  */
+    ADMM_OPT_COUNT = 10
 };
 int admm_set_option(int option, int value);
 int admm_get_option(int option, int* value);
@@ -251,7 +257,8 @@ int admm_get_option(int option, int* value);
 /* Which kernels a call runs (one decision table in admm_capi.hip, plan_paths; measurement and tests only).
  * mode: ADMM_MODE_FORWARD (admm_tvd_forward_*), ADMM_MODE_RECORD (admm_tvd_forward_record_*; flags =
  * its ADMM_REC_* word; its replay runs the sweep returned here), ADMM_MODE_BACKWARD (admm_tvd_backward_*;
- * want_hbar / want_rho = h_bar / rho_bar non-NULL).  kh = 0: no PSF.  *fwd_path = the forward's ADMM_PATH_*,
+ * want_hbar / want_rho = h_bar / rho_bar non-NULL).  kh = 0: no PSF.  planes = P * B of the call (0: not known,
+ * no plane-count rule, see ADMM_OPT_MIN_PLANES).  *fwd_path = the forward's ADMM_PATH_*,
  * *bwd_path = the reverse sweep's ADMM_PATH_SWEEP_* (0 for a plain forward).  The current library options
  * (admm_set_option) are taken into account; no GPU is touched.  The multi-branch entry points are not
  * covered (one grid of the fused kernels, or ADMM_E_UNSUPPORTED). */
@@ -272,8 +279,8 @@ enum {
     ADMM_PATH_SWEEP_RUNTIME_ISO = 13,
     ADMM_PATH_RESIDENT_ISO = 14       /* sides <= 256 isotropic: resident_iso_kernel + norm kernel per iteration */
 };
-int admm_query_paths(int M, int N, int iso, int kh, int mode, int flags, int want_hbar, int want_rho, int* fwd_path,
-                     int* bwd_path);
+int admm_query_paths(int M, int N, int iso, int kh, long long planes, int mode, int flags, int want_hbar, int want_rho,
+                     int* fwd_path, int* bwd_path);
 const char* admm_path_name(int path);
 
 /* Output transport of the batch-sharded solve (BASELINE c3; the reference gathers nothing -- its batch

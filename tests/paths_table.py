@@ -22,7 +22,10 @@ CASES = [
     ("250-iso-forward", 250, 250, True, 15, F, 0, False, False, {}, "smooth", None),
     ("480x640-forward", 640, 480, False, 15, F, 0, False, False, {}, "smooth", None),
     ("primes-forward", 37, 29, False, 5, F, 0, False, False, {}, "runtime", None),
-    ("128-forward", 128, 128, False, 15, F, 0, False, False, {}, "2pass", None),
+    ("128-forward", 128, 128, False, 15, F, 0, False, False, {}, "resident", None),
+    ("128-forward-RESIDENT0", 128, 128, False, 15, F, 0, False, False, {"RESIDENT": 0}, "2pass", None),
+    ("96-iso-forward", 96, 96, True, 0, F, 0, False, False, {}, "resident_iso", None),
+    ("32-iso-forward", 32, 32, True, 5, F, 0, False, False, {}, "resident_iso", None),
     ("128-forward-RESIDENT2", 128, 128, False, 15, F, 0, False, False, {"RESIDENT": 2}, "resident", None),
     ("demo32-record-RESIDENT2", 32, 32, False, 32, R, 0, False, False, {"RESIDENT": 2}, "resident", "sweep_2pass"),
     ("demo32-record-hbar-RESIDENT2", 32, 32, False, 32, R, HBAR, False, False, {"RESIDENT": 2}, "2pass", "sweep_2pass"),
@@ -52,4 +55,30 @@ CASES = [
     ("250-record-hbar", 250, 250, False, 15, R, HBAR, False, False, {}, "smooth", "sweep_runtime"),
     ("250-iso-backward", 250, 250, True, 15, B, 0, True, True, {}, "smooth", "sweep_runtime_iso"),
     ("primes-backward", 37, 29, False, 5, B, 0, True, True, {}, "runtime", "sweep_runtime"),
+]
+
+# The plane-count rule (ADMM_OPT_MIN_PLANES at its default, admm_capi.hip kMinPlanes): the one-workgroup-per-plane
+# paths from the measured batch sizes where they beat the 2-pass kernels.  The table above queries with planes = 0
+# (no rule), as its GPU test runs 2 planes with the rule off (conftest).
+# (id, M, N, iso, kh, mode, flags, want_hbar, want_rho, planes, expected forward, expected sweep)
+PLANE_CASES = [
+    ("c2-95", 256, 256, False, 15, F, 0, False, False, 95, "2pass", None),
+    ("c2-96", 256, 256, False, 15, F, 0, False, False, 96, "fused", None),
+    ("c5-record-masks-64", 256, 256, False, 0, R, MASKS, False, False, 64, "2pass", "sweep_2pass"),
+    ("c5-record-masks-96", 256, 256, False, 0, R, MASKS, False, False, 96, "fused", "sweep_fused"),
+    ("256-backward-norho-8", 256, 256, False, 15, B, 0, False, False, 8, "2pass", "sweep_2pass"),
+    ("iso256-forward-111", 256, 256, True, 15, F, 0, False, False, 111, "2pass_iso", None),
+    ("iso256-forward-112", 256, 256, True, 15, F, 0, False, False, 112, "fused_iso", None),
+    ("c5iso-record-masks-6", 256, 256, True, 0, R, MASKS, False, False, 6, "2pass_iso", "sweep_2pass_iso"),
+    ("c5iso-record-masks-128", 256, 256, True, 0, R, MASKS, False, False, 128, "fused_iso", "sweep_fused_iso"),
+    ("250-forward-128", 250, 250, False, 15, F, 0, False, False, 128, "smooth", None),
+    ("250-forward-192", 250, 250, False, 15, F, 0, False, False, 192, "resident", None),
+    ("250-record-64", 250, 250, False, 15, R, 0, False, False, 64, "smooth", "sweep_runtime"),
+    ("128-forward-191", 128, 128, False, 15, F, 0, False, False, 191, "2pass", None),
+    ("128-forward-192", 128, 128, False, 15, F, 0, False, False, 192, "resident", None),
+    ("96-forward-6", 96, 96, False, 0, F, 0, False, False, 6, "resident", None),
+    ("32-demo-forward-6", 32, 32, False, 32, F, 0, False, False, 6, "resident", None),
+    ("96-iso-forward-255", 96, 96, True, 0, F, 0, False, False, 255, "smooth", None),
+    ("96-iso-forward-256", 96, 96, True, 0, F, 0, False, False, 256, "resident_iso", None),
+    ("32-iso-forward-6", 32, 32, True, 5, F, 0, False, False, 6, "2pass_iso", None),
 ]

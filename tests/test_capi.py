@@ -181,10 +181,13 @@ def test_multi_branch_workspace_and_validation():
     masks = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_RECORD | _lib.REC_MASKS)
     planes, px = 5 * 3 * 64, 256 * 256
     assert full - plain >= 49 * planes * px * 8 and masks - plain < 49 * planes * px * 8 / 8
-    # the single-solve recording with ADMM_REC_MASKS is sized for the mask trajectory too
-    f = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, 0)
-    m = _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, _lib.REC_MASKS)
+    # the single-solve recording with ADMM_REC_MASKS is sized for the mask trajectory too (from the fused
+    # path's plane count on; 6 planes record for the 2-pass sweep, which takes no mask bits)
+    f = _lib.backward_workspace_bytes(256, 256, 3, 32, 0, 0, False, 50, 0)
+    m = _lib.backward_workspace_bytes(256, 256, 3, 32, 0, 0, False, 50, _lib.REC_MASKS)
     assert m < f
+    assert _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, _lib.REC_MASKS) == \
+        _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, False, 50, 0)
     # isotropic (ADMM_MULTI_ISO): f maps and q partials on top of the plain layout; a recording keeps s_k
     # itself (the BT derivative needs it), |s_k| per branch and the R maps -- ADMM_REC_MASKS does not shrink it
     iso = _lib.multi_workspace_bytes(256, 256, 3, 64, 5, 50, _lib.MULTI_ISO)
@@ -208,3 +211,24 @@ def test_path_decision_table(case):
         for k, v in opts.items():
             st.enter_context(_lib.option(k, v))
         assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho) == (fwd, bwd), cid
+
+
+@pytest.mark.parametrize("case", __import__("paths_table").PLANE_CASES,
+                         ids=[c[0] for c in __import__("paths_table").PLANE_CASES])
+def test_path_decision_table_plane_count_rule(case):
+    """Small batches go to the 2-pass kernels (ADMM_OPT_MIN_PLANES = -1, the default); 0 switches the rule off and
+    a positive value sets one threshold for every per-plane path."""
+    cid, M, N, iso, kh, mode, flags, hb, rho, planes, fwd, bwd = case
+    assert _lib.get_option("MIN_PLANES") == -1
+    assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho, planes) == (fwd, bwd), cid
+    with _lib.option("MIN_PLANES", 0):
+        assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho, planes) == \
+            _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho, 0), cid
+    with _lib.option("MIN_PLANES", planes + 1):
+        small = _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho, planes)
+        assert small[0] not in ("fused", "fused_iso", "resident", "resident_iso"), cid
+
+
+def test_query_paths_rejects_negative_planes():
+    with pytest.raises(Exception):
+        _lib.query_paths(256, 256, False, 0, 0, 0, False, False, -1)

@@ -48,6 +48,8 @@ def _worker(rank, world, port, q, case, n_local, chunks, engine, distinct):
 
 def _work(rank, world, port, q, case, n_local, chunks, engine, distinct):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from admm_deconv import _lib
+    _lib.set_option("MIN_PLANES", 0)   # the parent's reference solve runs the per-plane kernels too (conftest)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)

@@ -33,6 +33,7 @@ def _worker(rank, world, port, q, M, need_rho, resident=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from admm_deconv import _lib
     _lib.set_option("RESIDENT", resident if resident else 1)
+    _lib.set_option("MIN_PLANES", 0)   # the parent's reference solve runs the per-plane kernels too (conftest)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     h, y, xbar = _inputs(M)

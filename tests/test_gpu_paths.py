@@ -13,7 +13,7 @@ import torch
 
 import admm_deconv
 from admm_deconv import _lib, synth
-from paths_table import CASES, HBAR, MASKS
+from paths_table import CASES, HBAR, MASKS, PLANE_CASES
 
 pytestmark = pytest.mark.gpu
 K = 4
@@ -23,31 +23,26 @@ def _counts():
     return {name: _lib.profile_get(cls)[1] for cls, name in _lib.KERNEL_CLASSES.items()}
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_launched_kernels_follow_the_decision_table(dev, case):
-    cid, M, N, iso, kh, mode, flags, hb, rho, opts, fwd, bwd = case
+def _run_and_check(dev, cid, M, N, iso, kh, mode, flags, hb, rho, planes, fwd, bwd):
     h = synth.gaussian_psf(kh, 1.0) if kh else None
     ht = None if h is None else torch.from_numpy(h).to(dev)
-    y = torch.from_numpy(synth.make_batch(2, M, N, h)).to(dev)
+    y = torch.from_numpy(synth.make_batch(planes, M, N, h)).to(dev)
     xb = torch.randn_like(y)
-    with contextlib.ExitStack() as st:
-        for k, v in opts.items():
-            st.enter_context(_lib.option(k, v))
-        assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho) == (fwd, bwd), cid
-        _lib.profile_reset()
-        _lib.profile_enable(True)
-        try:
-            if mode == 0:
-                admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, iso, K)
-            elif mode == 1:
-                x, rec = admm_deconv.tvd_fft_record(y, 0.0041, 0.021, ht, iso, K, need_h=bool(flags & HBAR),
-                                                    need_rho=not flags & MASKS)
-                admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_rho=not flags & MASKS)
-            else:
-                admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, ht, iso, K, need_h=hb, need_rho=rho)
-            torch.cuda.synchronize()
-        finally:
-            _lib.profile_enable(False)
+    assert _lib.query_paths(M, N, iso, kh, mode, flags, hb, rho, planes) == (fwd, bwd), cid
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    try:
+        if mode == 0:
+            admm_deconv.tvd_fft(y, 0.0041, 0.021, ht, iso, K)
+        elif mode == 1:
+            x, rec = admm_deconv.tvd_fft_record(y, 0.0041, 0.021, ht, iso, K, need_h=bool(flags & HBAR),
+                                                need_rho=not flags & MASKS)
+            admm_deconv.tvd_fft_backward_recorded(rec, x, xb, need_rho=not flags & MASKS)
+        else:
+            admm_deconv.tvd_fft_backward(y, xb, 0.0041, 0.021, ht, iso, K, need_h=hb, need_rho=rho)
+        torch.cuda.synchronize()
+    finally:
+        _lib.profile_enable(False)
     c = _counts()
     plane, adj, col = c.get("plane", 0), c.get("adjoint", 0), c.get("column", 0)
     want_plane = {"fused": 1, "resident": 1, "fused_iso": K, "resident_iso": K}.get(fwd, 0)
@@ -60,3 +55,22 @@ def test_launched_kernels_follow_the_decision_table(dev, case):
         assert adj >= K - 1 and col > 0, f"{cid}: {c}"
     if fwd not in ("fused", "resident", "fused_iso", "resident_iso"):
         assert col >= K, f"{cid}: {c}"
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_launched_kernels_follow_the_decision_table(dev, case):
+    """2 planes, the plane-count rule off (conftest), options as the table gives them."""
+    cid, M, N, iso, kh, mode, flags, hb, rho, opts, fwd, bwd = case
+    with contextlib.ExitStack() as st:
+        for k, v in opts.items():
+            st.enter_context(_lib.option(k, v))
+        _run_and_check(dev, cid, M, N, iso, kh, mode, flags, hb, rho, 2, fwd, bwd)
+
+
+@pytest.mark.min_planes_rule
+@pytest.mark.parametrize("case", PLANE_CASES, ids=[c[0] for c in PLANE_CASES])
+def test_launched_kernels_follow_the_plane_count_rule(dev, case):
+    """The library's defaults: below the measured plane counts the 2-pass kernels run (ADMM_OPT_MIN_PLANES = -1)."""
+    cid, M, N, iso, kh, mode, flags, hb, rho, planes, fwd, bwd = case
+    assert _lib.get_option("MIN_PLANES") == -1
+    _run_and_check(dev, cid, M, N, iso, kh, mode, flags, hb, rho, planes, fwd, bwd)
