@@ -377,7 +377,9 @@ struct PathIn {
 //   fused_iso 256^2          128: 2.03 vs 2.13, 64: 1.84 vs 1.40  -> 112
 //   resident 250^2           192: 2.53 vs 2.96, 128: 2.48 vs 1.99; 128^2 256: 0.88 vs 0.93, 128: 0.84 vs 0.62
 //                            -> 192 for sides >= 128 (smaller sides: every batch, the per-plane latency is small)
-//   resident_iso             96^2 x 256 0.93 vs 1.17, 32^2 x 512 0.57 vs 0.69; 128^2 x 192 1.45 vs 0.99 -> 256
+//                            (sides < 128: 96^2 0.43 vs 0.40 at 1..16 planes, 64^2 and 32^2 faster at every count)
+//   resident_iso             256 planes: 250^2 5.10 vs 5.64, 120^2 1.28 vs 1.52, 64^2 0.56 vs 0.60; 128^2 x 192
+//                            1.45 vs 0.99, 250^2 x 64 4.41 vs 1.84  -> 256
 enum MinPlanesFor { kMinFused, kMinFusedIso, kMinResident, kMinResidentIso };
 bool enough_planes(const PathIn& q, MinPlanesFor which) {
     const int o = opt(ADMM_OPT_MIN_PLANES);

@@ -978,11 +978,12 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
 // 0.61 vs 1.59; profiles/r04_resident_pow2.jsonl).  Small batches are left to the 2-pass kernels by plan_paths.
 #define RS_SLOWER(X)
 
-// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster, or that are not
-// measured yet (profiles/r04_resident_iso.jsonl: 96^2 x 256 0.93 vs 1.17 ms and 32^2 x 512 0.57 vs 0.69 resident;
-// 128^2 x 192 1.45 vs 0.99 and 250^2 x 64 4.41 vs 1.84 2-pass -- one launch per iteration with one plane per CU
-// needs a full wave of planes)
-#define RS_ISO_SLOWER(X) X(250, 250) X(240, 240) X(200, 200) X(192, 192) X(160, 160) X(128, 128) X(120, 120) X(64, 64)
+// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster.  None at a full
+// wave of planes (profiles/r04_resident_iso.jsonl, r04_small_batch_paths.jsonl; 256 planes: 250^2 5.10 vs 5.64 ms,
+// 200^2 3.20 vs 3.41, 160^2 2.10 vs 2.27, 120^2 1.28 vs 1.52, 96^2 0.93 vs 1.17, 64^2 0.56 vs 0.60; 32^2 x 512 0.57
+// vs 0.69).  Below a wave the 2-pass kernels win (one launch per iteration with one plane per CU: 250^2 x 64 4.41
+// vs 1.84, 128^2 x 192 1.45 vs 0.99), which plan_paths' plane-count rule leaves to them.
+#define RS_ISO_SLOWER(X)
 
 bool has_iso_shape(int M, int N, bool all) {
 #define X(m, n) \

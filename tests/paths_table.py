@@ -19,7 +19,8 @@ CASES = [
     ("96-forward", 96, 96, False, 0, F, 0, False, False, {}, "resident", None),
     ("250-forward-RESIDENT0", 250, 250, False, 15, F, 0, False, False, {"RESIDENT": 0}, "smooth", None),
     ("250-forward-SMOOTH0", 250, 250, False, 15, F, 0, False, False, {"SMOOTH": 0}, "runtime", None),
-    ("250-iso-forward", 250, 250, True, 15, F, 0, False, False, {}, "smooth", None),
+    ("250-iso-forward", 250, 250, True, 15, F, 0, False, False, {}, "resident_iso", None),
+    ("250-iso-forward-RESIDENT0", 250, 250, True, 15, F, 0, False, False, {"RESIDENT": 0}, "smooth", None),
     ("480x640-forward", 640, 480, False, 15, F, 0, False, False, {}, "smooth", None),
     ("primes-forward", 37, 29, False, 5, F, 0, False, False, {}, "runtime", None),
     ("128-forward", 128, 128, False, 15, F, 0, False, False, {}, "resident", None),
@@ -80,5 +81,7 @@ PLANE_CASES = [
     ("32-demo-forward-6", 32, 32, False, 32, F, 0, False, False, 6, "resident", None),
     ("96-iso-forward-255", 96, 96, True, 0, F, 0, False, False, 255, "smooth", None),
     ("96-iso-forward-256", 96, 96, True, 0, F, 0, False, False, 256, "resident_iso", None),
+    ("250-iso-forward-255", 250, 250, True, 15, F, 0, False, False, 255, "smooth", None),
+    ("250-iso-forward-256", 250, 250, True, 15, F, 0, False, False, 256, "resident_iso", None),
     ("32-iso-forward-6", 32, 32, True, 5, F, 0, False, False, 6, "2pass_iso", None),
 ]
