@@ -313,7 +313,13 @@ struct Geo {
     static constexpr int NLC = nlc();              // line chunks
     static constexpr int TL = tl(NLC);             // lines per line chunk
     static constexpr int BUF = imax(KBC * FS, (TL / 2 + 2) * MM);
-    static constexpr size_t lds_bytes() { return (size_t)(MM + NN + BUF) * 8; }
+    // LDS rows for each wave's first and last row update (interleaved like a line pair: 2 M floats per wave), so
+    // that the row step writes every v through one uniform address select instead of holding those two rows in
+    // registers under branches (the neighbouring waves read the x they replace until the block barrier).  Only
+    // where it fits beside the geometry above (not at 192^2, whose single line chunk fills the LDS).
+    static constexpr int SCR = 8 * MM;             // float2 slots
+    static constexpr bool kScr = (size_t)(MM + NN + BUF + SCR) * 8 + 512 <= (size_t)kLdsBytes;
+    static constexpr size_t lds_bytes() { return (size_t)(MM + NN + BUF + (kScr ? SCR : 0)) * 8; }
     static_assert(MM % 2 == 0 && NN % 2 == 0 && MM <= 256 && NN <= 256, "resident kernel: even M, N <= 256");
     static_assert(NCC >= 1 && NLC >= 1, "resident kernel: shape does not fit one CU");
     static_assert(LS % 2 == 0 && TL % 2 == 0, "line pairs within a lane pair");
@@ -632,7 +638,8 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         const int lane = t & 63;
         const int ua = 2 + (w * T) / 8, ub = 1 + ((w + 1) * T) / 8;
         const float tau = a.tau, rho = a.rho;
-        const rsrc_t rso = make_rsrc(a.so, 2 * MN * 4), rsn = make_rsrc(a.sn, 2 * MN * 4), rh = make_rsrc(a.hty, MN * 4);
+        const rsrc_t rso = make_rsrc(a.so, a.first ? 0u : 2 * MN * 4), rsn = make_rsrc(a.sn, 2 * MN * 4),
+                     rh = make_rsrc(a.hty, MN * 4), rnone = make_rsrc(a.sn, 0u);
         // float offsets of pixel i and its neighbours within a pair row (LDS), byte offset of i + 1 (HBM)
         // (left and right neighbour offsets packed in one register: 16 bits each)
         int pc[QN], plr[QN];
@@ -645,6 +652,13 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         const unsigned gl = 4u * (unsigned)lane;   // + 256 q: the instruction's immediate offset
         auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
         auto valid = [&](int q) { return q < QN - 1 || lane + 64 * q < MM; };
+        // HBM stores of lanes past the row's last pixel go to a lane offset beyond the buffer (dropped by the
+        // buffer unit): no exec-mask branch around them
+        const unsigned glst = lane + 64 * (QN - 1) < MM ? gl : 0x80000000u;
+        auto gst = [&](int q) { return q < QN - 1 ? gl : glst; };
+        // the wave's scratch rows (float offsets from Xf): first row at + 0, last row at + 1, stride 2 like a pair
+        constexpr bool SC = G::kScr;
+        const int scr = 2 * G::BUF + w * 2 * MM;
         float vf[QN], vl[QN];
 #ifdef RS_SKIP_ROWS   // timing experiments only: no row update (wrong results)
         if (false) {
@@ -658,15 +672,16 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                 const unsigned so = 4u * (unsigned)(j * MM);
 #pragma unroll
                 for (int q = 0; q < QN; ++q) {
-                    const float o = a.first ? 0.0f : bld1(rso, gl + 256 * q, so);
+                    const float o = bld1(rso, gl + 256 * q, so);
                     const float s0 = (Xf[ru + pc[q]] - Xf[rm + pc[q]]) + clipf(o, tau);
-                    if (valid(q)) bst1(rsn, gl + 256 * q, so, s0);
+                    bst1(rsn, gst(q) + 256 * q, so, s0);
                     w0c[q] = prox_w(s0, tau);
                 }
             }
             struct GIn {
                 float a0n, a1, h;
             };
+            // (the first iteration reads s_old through a zero-size resource: every load returns 0, no branch)
             auto gload = [&](GIn (&g)[QN], int u) {
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
@@ -674,24 +689,11 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
 #pragma unroll
                 for (int q = 0; q < QN; ++q) {
                     g[q].h = bld1(rh, gl + 256 * q, oj);
-                    if (!a.first) {
-                        g[q].a0n = bld1(rso, gl + 256 * q, on);
-                        g[q].a1 = bld1(rso, gl + 256 * q, oj + 4 * MN);
-                    } else {
-                        g[q].a0n = g[q].a1 = 0.0f;
-                    }
+                    g[q].a0n = bld1(rso, gl + 256 * q, on);
+                    g[q].a1 = bld1(rso, gl + 256 * q, oj + 4 * MN);
                 }
             };
-            // rows u + 1 .. u + RS_PD in flight while row u is computed (loads past the chunk read rows the
-            // next chunk or another wave owns, or beyond the plane, where the buffer returns 0: never used)
-            GIn pf[RS_PD][QN];
-#pragma unroll
-            for (int d = 0; d < RS_PD; ++d) gload(pf[d], ua + d);
-#pragma unroll 1
-            for (int u = ua; u <= ub; ++u) {
-                GIn nx[QN];
-                gload(nx, u + RS_PD);
-                GIn (&cur)[QN] = pf[0];
+            auto step = [&](int u, const GIn (&cur)[QN]) {
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
                 const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
@@ -727,24 +729,43 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                     const float s0n = (xn - xc) + clipf(cur[q].a0n, tau);
                     const float w0n = prox_w(s0n, tau);
                     const float s1 = (xc - xl) + clipf(cur[q].a1, tau);
-                    if (valid(q)) {
-                        if (u < ub) bst1(rsn, gl + 256 * q, on, s0n);
-                        bst1(rsn, gl + 256 * q, oj + 4 * MN, s1);
-                    }
+                    // s0 of line j + 1: the next wave's (or chunk's) first row, which it stores itself -- not
+                    // from the last row (a zero-size resource drops the store)
+                    bst1(u < ub ? rsn : rnone, gst(q) + 256 * q, on, s0n);
+                    bst1(rsn, gst(q) + 256 * q, oj + 4 * MN, s1);
                     const float w1 = prox_w(s1, tau);
                     const float w1r = prox_w((xr - xc) + clipf(a1r[q], tau), tau);
                     const float v = fmaf(rho, (w0c[q] - w0n) + (w1 - w1r), cur[q].h);
                     w0c[q] = w0n;
-                    if (u == ua) vf[q] = v;
-                    else if (u == ub) vl[q] = v;
-                    else if (valid(q)) Xf[ru + pc[q]] = v;
+                    if constexpr (SC) {
+                        const int rd = u == ua ? scr : u == ub ? scr + 1 : ru;   // uniform: a scalar select
+                        if (valid(q)) Xf[rd + pc[q]] = v;
+                    } else {
+                        if (u == ua) vf[q] = v;
+                        else if (u == ub) vl[q] = v;
+                        else if (valid(q)) Xf[ru + pc[q]] = v;
+                    }
                 }
+            };
+            // rows u + 1 .. u + RS_PD in flight while row u is computed (loads past the chunk read rows the
+            // next chunk or another wave owns, or beyond the plane, where the buffer returns 0: never used).
+            // RS_PD + 1 ring slots, the loop unrolled by that many rows: row ua + i lives in slot i % NS, a
+            // compile-time index in every unrolled step, so the ring never moves a register (rotating it
+            // cost 77 v_mov per row, a third of the row's VALU)
+            constexpr int NS = RS_PD + 1;
+            GIn pf[NS][QN];
 #pragma unroll
-                for (int d = 0; d + 1 < RS_PD; ++d)
-#pragma unroll
-                    for (int q = 0; q < QN; ++q) pf[d][q] = pf[d + 1][q];
-#pragma unroll
-                for (int q = 0; q < QN; ++q) pf[RS_PD - 1][q] = nx[q];
+            for (int d = 0; d < RS_PD; ++d) gload(pf[d], ua + d);
+#pragma unroll 1
+            for (int u0 = ua; u0 <= ub; u0 += NS) {
+                static_for<0, NS>([&](auto id) {
+                    constexpr int d = decltype(id)::value;
+                    const int u = u0 + d;
+                    if (u <= ub) {
+                        gload(pf[(d + RS_PD) % NS], u + RS_PD);
+                        step(u, pf[d]);
+                    }
+                });
             }
         }
         __syncthreads();
@@ -752,8 +773,8 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
 #pragma unroll
             for (int q = 0; q < QN; ++q) {
                 if (valid(q)) {
-                    Xf[row(ua) + pc[q]] = vf[q];
-                    if (ub > ua) Xf[row(ub) + pc[q]] = vl[q];
+                    Xf[row(ua) + pc[q]] = SC ? Xf[scr + pc[q]] : vf[q];
+                    if (ub > ua) Xf[row(ub) + pc[q]] = SC ? Xf[scr + 1 + pc[q]] : vl[q];
                 }
             }
         }

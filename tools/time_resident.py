@@ -31,7 +31,7 @@ if len(sys.argv) > 1:
 
 
 def solve(y, h, K, resident):
-    with _lib.option("RESIDENT", 2 * int(resident)):   # 2: every compiled shape
+    with _lib.option("RESIDENT", 2 * int(resident)), _lib.option("MIN_PLANES", 0):   # 2: every compiled shape, any batch
         x = admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, ISO, K)
     torch.cuda.synchronize()
     return x
@@ -72,7 +72,7 @@ def main():
                 solve(y, h, K, res)
             reps = 5
             t0 = time.perf_counter()
-            with _lib.option("RESIDENT", 2 * int(res)):
+            with _lib.option("RESIDENT", 2 * int(res)), _lib.option("MIN_PLANES", 0):
                 for _ in range(reps):
                     admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, ISO, K)
             torch.cuda.synchronize()
