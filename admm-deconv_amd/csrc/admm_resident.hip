@@ -77,6 +77,33 @@ __device__ __forceinline__ float bld1(rsrc_t r, unsigned vo, unsigned so) {
 __device__ __forceinline__ void bst1(rsrc_t r, unsigned vo, unsigned so, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
 }
+using u32x2 = unsigned __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 bld2(rsrc_t r, unsigned vo, unsigned so) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+__device__ __forceinline__ void bst2(rsrc_t r, unsigned vo, unsigned so, float2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
+}
+// G neighbouring floats of one lane, moved by one buffer access
+template <int G>
+struct Vg {
+    float v[G];
+    static __device__ __forceinline__ Vg load(rsrc_t r, unsigned vo, unsigned so) {
+        Vg x;
+        if constexpr (G == 2) {
+            const float2 f = bld2(r, vo, so);
+            x.v[0] = f.x;
+            x.v[1] = f.y;
+        } else {
+            x.v[0] = bld1(r, vo, so);
+        }
+        return x;
+    }
+    __device__ __forceinline__ void store(rsrc_t r, unsigned vo, unsigned so) const {
+        if constexpr (G == 2) bst2(r, vo, so, make_float2(v[0], v[1]));
+        else bst1(r, vo, so, v[0]);
+    }
+};
 
 // The thread index through an opaque move: values derived from it are recomputed inside the iteration loop
 // rather than hoisted out of it (dozens of per-pass start indices and LDS bases would otherwise stay live
@@ -303,6 +330,8 @@ struct Geo {
     static constexpr int NREG = NCC * NR;          // spectrum registers (float2) per thread
     static constexpr int FS = RC ? (NN | 1) : fs(NCC);
     static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
+    static constexpr int GP = MM > 64 ? 2 : 1;     // neighbouring pixels per lane in the row update
+    static constexpr int QG = cdiv(MM, 64 * GP);   // slices of 64 lanes per row
     // line chunks: TL lines (a multiple of LS: whole registers) + a halo pair either side, as complex pairs
     static constexpr int tl(int n) { return cdiv(cdiv(NN, n), LS) * LS; }
     static constexpr int nlc() {
@@ -629,10 +658,17 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
 
     if constexpr (MODE == kUpdate) {
         // ---- row update: wave w walks staged lines ua .. ub (staged line u = line jc0 + u - 2) ----
-        // Global traffic through buffer resources: the row offset is wave-uniform (soffset), the lane's
-        // pixel offset a per-lane constant (voffset), so no 64-bit address per load.
-        constexpr int QN = G::QN;
+        // A lane takes GP neighbouring pixels i0 = GP (lane + 64 q) .. i0 + GP - 1 (GP = 2 for lines longer than
+        // 64: 8-byte buffer loads and stores, so a row costs 3 loads + 2 stores per slice of 128 pixels).  gfx950
+        // counts loads and stores in one 6-bit vmcnt, so at most 63 of them are in flight per wave: with 4-byte
+        // accesses that held about 3 rows ahead and the update ran at the HBM latency per 3 rows (pairs: 250^2
+        // 2.68 -> 2.62 ms, 240^2 3.11 -> 2.43, 192^2 1.73 -> 1.42, 128^2 0.78 -> 0.70; at 64 and 32 points a
+        // pair per lane leaves half the lanes idle: 0.59 -> 0.66 and 0.50 -> 0.64, so those keep GP = 1).
+        // Global traffic through buffer resources: the row offset is wave-uniform (soffset), the lane's pixel
+        // offset a per-lane constant (voffset).
+        constexpr int GP = G::GP, QG = G::QG;
         constexpr unsigned MN = (unsigned)MM * NN;
+        using PV = Vg<GP>;
         const int t = tid();
         const int w = __builtin_amdgcn_readfirstlane(t >> 6);
         const int lane = t & 63;
@@ -640,110 +676,136 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         const float tau = a.tau, rho = a.rho;
         const rsrc_t rso = make_rsrc(a.so, a.first ? 0u : 2 * MN * 4), rsn = make_rsrc(a.sn, 2 * MN * 4),
                      rh = make_rsrc(a.hty, MN * 4), rnone = make_rsrc(a.sn, 0u);
-        // float offsets of pixel i and its neighbours within a pair row (LDS), byte offset of i + 1 (HBM)
-        // (left and right neighbour offsets packed in one register: 16 bits each)
-        int pc[QN], plr[QN];
+        // LDS float offsets (x at dpos order within a pair row) of the lane's pixels and of the first one's left
+        // neighbour (the others' left neighbours are the lane's own pixels)
+        int po[QG][GP], plo[QG];
 #pragma unroll
-        for (int q = 0; q < QN; ++q) {
-            const int i = lane + 64 * q < MM ? lane + 64 * q : 0;
-            pc[q] = 2 * dpos<MM>(i);
-            plr[q] = 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1) | (2 * dpos<MM>(i + 1 == MM ? 0 : i + 1)) << 16;
+        for (int q = 0; q < QG; ++q) {
+            const int i0 = GP * (lane + 64 * q) < MM ? GP * (lane + 64 * q) : 0;
+#pragma unroll
+            for (int g = 0; g < GP; ++g) po[q][g] = 2 * dpos<MM>(i0 + g);
+            plo[q] = 2 * dpos<MM>(i0 == 0 ? MM - 1 : i0 - 1);
         }
-        const unsigned gl = 4u * (unsigned)lane;   // + 256 q: the instruction's immediate offset
+        constexpr unsigned SL = 256 * GP;                    // bytes per slice: the instruction's immediate offset
+        const unsigned gl = 4u * GP * (unsigned)lane;
         auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
-        auto valid = [&](int q) { return q < QN - 1 || lane + 64 * q < MM; };
-        // HBM stores of lanes past the row's last pixel go to a lane offset beyond the buffer (dropped by the
-        // buffer unit): no exec-mask branch around them
-        const unsigned glst = lane + 64 * (QN - 1) < MM ? gl : 0x80000000u;
-        auto gst = [&](int q) { return q < QN - 1 ? gl : glst; };
+        auto valid = [&](int q) { return q < QG - 1 || GP * (lane + 64 * q) < MM; };
+        // HBM stores of lanes past the row's end go to a lane offset beyond the buffer (dropped by the buffer
+        // unit): no exec-mask branch around them
+        const unsigned glst = GP * (lane + 64 * (QG - 1)) < MM ? gl : 0x80000000u;
+        auto gst = [&](int q) { return q < QG - 1 ? gl : glst; };
+        auto ld = [&](rsrc_t r, int q, unsigned so) { return PV::load(r, gl + SL * q, so); };
+        auto st = [&](rsrc_t r, int q, unsigned so, const PV& v) { v.store(r, gst(q) + SL * q, so); };
+        auto xget = [&](int rbase, int q) {
+            PV x;
+#pragma unroll
+            for (int g = 0; g < GP; ++g) x.v[g] = Xf[rbase + po[q][g]];
+            return x;
+        };
+        auto put = [&](int q, int rbase, const PV& v) {
+            if (valid(q)) {
+#pragma unroll
+                for (int g = 0; g < GP; ++g) Xf[rbase + po[q][g]] = v.v[g];
+            }
+        };
         // the wave's scratch rows (float offsets from Xf): first row at + 0, last row at + 1, stride 2 like a pair
         constexpr bool SC = G::kScr;
         const int scr = 2 * G::BUF + w * 2 * MM;
-        float vf[QN], vl[QN];
+        PV vf[QG], vl[QG];
 #ifdef RS_SKIP_ROWS   // timing experiments only: no row update (wrong results)
         if (false) {
 #else
         if (ub >= ua) {
 #endif
-            float w0c[QN];
+            PV w0c[QG];
             {
                 const int j = jc0 + ua - 2;
                 const int ru = row(ua), rm = row(ua - 1);
                 const unsigned so = 4u * (unsigned)(j * MM);
 #pragma unroll
-                for (int q = 0; q < QN; ++q) {
-                    const float o = bld1(rso, gl + 256 * q, so);
-                    const float s0 = (Xf[ru + pc[q]] - Xf[rm + pc[q]]) + clipf(o, tau);
-                    bst1(rsn, gst(q) + 256 * q, so, s0);
-                    w0c[q] = prox_w(s0, tau);
+                for (int q = 0; q < QG; ++q) {
+                    const PV o = ld(rso, q, so), xa = xget(ru, q), xb = xget(rm, q);
+                    PV s0;
+#pragma unroll
+                    for (int g = 0; g < GP; ++g) s0.v[g] = (xa.v[g] - xb.v[g]) + clipf(o.v[g], tau);
+                    st(rsn, q, so, s0);
+#pragma unroll
+                    for (int g = 0; g < GP; ++g) w0c[q].v[g] = prox_w(s0.v[g], tau);
                 }
             }
             struct GIn {
-                float a0n, a1, h;
+                PV a0n, a1, h;
             };
             // (the first iteration reads s_old through a zero-size resource: every load returns 0, no branch)
-            auto gload = [&](GIn (&g)[QN], int u) {
+            auto gload = [&](GIn (&gi)[QG], int u) {
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
                 const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
 #pragma unroll
-                for (int q = 0; q < QN; ++q) {
-                    g[q].h = bld1(rh, gl + 256 * q, oj);
-                    g[q].a0n = bld1(rso, gl + 256 * q, on);
-                    g[q].a1 = bld1(rso, gl + 256 * q, oj + 4 * MN);
+                for (int q = 0; q < QG; ++q) {
+                    gi[q].h = ld(rh, q, oj);
+                    gi[q].a0n = ld(rso, q, on);
+                    gi[q].a1 = ld(rso, q, oj + 4 * MN);
                 }
             };
-            auto step = [&](int u, const GIn (&cur)[QN]) {
+            auto step = [&](int u, const GIn (&cur)[QG]) {
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
                 const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
                 const int ru = row(u), rn = row(u + 1);
-                // every read of the row before any v is written over it: lanes read their neighbours'
-                // pixels, which other q slices of the same wave overwrite
-                float xcq[QN], xnq[QN], xlq[QN], xrq[QN];
+                // every read of the row before any v is written over it: lanes read their neighbours' pixels
+                PV xc[QG], xn[QG];
+                float xl[QG];
 #pragma unroll
-                for (int q = 0; q < QN; ++q) {
-                    xcq[q] = Xf[ru + pc[q]];
-                    xnq[q] = Xf[rn + pc[q]];
-                    xlq[q] = Xf[ru + (plr[q] & 0xffff)];
-                    xrq[q] = Xf[ru + (plr[q] >> 16)];
+                for (int q = 0; q < QG; ++q) {
+                    xc[q] = xget(ru, q);
+                    xn[q] = xget(rn, q);
+                    xl[q] = Xf[ru + plo[q]];
                 }
-                // s_old channel 1 of pixel i + 1: the next lane's (lane 63: lane 0 of the next slice; the
-                // last pixel wraps to pixel 0), through ds_bpermute instead of a second load
-                float a1r[QN];
-                {
-                    float sh[QN];
+                PV w0n[QG], w1[QG];
 #pragma unroll
-                    for (int q = 0; q < QN; ++q)
-                        sh[q] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * ((lane + 1) & 63), __float_as_int(cur[q].a1)));
-                    const float p0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cur[0].a1)));
+                for (int q = 0; q < QG; ++q) {
+                    PV s0n, s1;
 #pragma unroll
-                    for (int q = 0; q < QN; ++q) {
-                        const float nx1 = q + 1 < QN ? sh[q + 1 < QN ? q + 1 : q] : p0;
-                        a1r[q] = lane + 64 * q + 1 == MM ? p0 : (lane == 63 ? nx1 : sh[q]);
+                    for (int g = 0; g < GP; ++g) {
+                        s0n.v[g] = (xn[q].v[g] - xc[q].v[g]) + clipf(cur[q].a0n.v[g], tau);
+                        s1.v[g] = (xc[q].v[g] - (g == 0 ? xl[q] : xc[q].v[g > 0 ? g - 1 : 0])) + clipf(cur[q].a1.v[g], tau);
                     }
-                }
-#pragma unroll
-                for (int q = 0; q < QN; ++q) {
-                    const float xc = xcq[q], xn = xnq[q], xl = xlq[q], xr = xrq[q];
-                    const float s0n = (xn - xc) + clipf(cur[q].a0n, tau);
-                    const float w0n = prox_w(s0n, tau);
-                    const float s1 = (xc - xl) + clipf(cur[q].a1, tau);
                     // s0 of line j + 1: the next wave's (or chunk's) first row, which it stores itself -- not
                     // from the last row (a zero-size resource drops the store)
-                    bst1(u < ub ? rsn : rnone, gst(q) + 256 * q, on, s0n);
-                    bst1(rsn, gst(q) + 256 * q, oj + 4 * MN, s1);
-                    const float w1 = prox_w(s1, tau);
-                    const float w1r = prox_w((xr - xc) + clipf(a1r[q], tau), tau);
-                    const float v = fmaf(rho, (w0c[q] - w0n) + (w1 - w1r), cur[q].h);
-                    w0c[q] = w0n;
+                    st(u < ub ? rsn : rnone, q, on, s0n);
+                    st(rsn, q, oj + 4 * MN, s1);
+#pragma unroll
+                    for (int g = 0; g < GP; ++g) {
+                        w0n[q].v[g] = prox_w(s0n.v[g], tau);
+                        w1[q].v[g] = prox_w(s1.v[g], tau);
+                    }
+                }
+                // w of channel 1 at the pixel right of each: the lane's own next pixel, and for its last pixel the
+                // next lane's first (lane 63: lane 0 of the next slice; the row's last pixel wraps to pixel 0) --
+                // the value the neighbour computed, not a second evaluation of it
+                float sh[QG];
+#pragma unroll
+                for (int q = 0; q < QG; ++q)
+                    sh[q] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * ((lane + 1) & 63), __float_as_int(w1[q].v[0])));
+                const float p0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(w1[0].v[0])));
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    const float nx = q + 1 < QG ? sh[q + 1 < QG ? q + 1 : q] : p0;
+                    const float wlast = GP * (lane + 64 * q) + GP == MM ? p0 : (lane == 63 ? nx : sh[q]);
+                    PV v;
+#pragma unroll
+                    for (int g = 0; g < GP; ++g) {
+                        const float w1r = g + 1 < GP ? w1[q].v[g + 1 < GP ? g + 1 : g] : wlast;
+                        v.v[g] = fmaf(rho, (w0c[q].v[g] - w0n[q].v[g]) + (w1[q].v[g] - w1r), cur[q].h.v[g]);
+                    }
+                    w0c[q] = w0n[q];
                     if constexpr (SC) {
-                        const int rd = u == ua ? scr : u == ub ? scr + 1 : ru;   // uniform: a scalar select
-                        if (valid(q)) Xf[rd + pc[q]] = v;
+                        put(q, u == ua ? scr : u == ub ? scr + 1 : ru, v);   // uniform: a scalar select
                     } else {
                         if (u == ua) vf[q] = v;
                         else if (u == ub) vl[q] = v;
-                        else if (valid(q)) Xf[ru + pc[q]] = v;
+                        else put(q, ru, v);
                     }
                 }
             };
@@ -753,7 +815,7 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
             // compile-time index in every unrolled step, so the ring never moves a register (rotating it
             // cost 77 v_mov per row, a third of the row's VALU)
             constexpr int NS = RS_PD + 1;
-            GIn pf[NS][QN];
+            GIn pf[NS][QG];
 #pragma unroll
             for (int d = 0; d < RS_PD; ++d) gload(pf[d], ua + d);
 #pragma unroll 1
@@ -771,11 +833,9 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         __syncthreads();
         if (ub >= ua) {
 #pragma unroll
-            for (int q = 0; q < QN; ++q) {
-                if (valid(q)) {
-                    Xf[row(ua) + pc[q]] = SC ? Xf[scr + pc[q]] : vf[q];
-                    if (ub > ua) Xf[row(ub) + pc[q]] = SC ? Xf[scr + 1 + pc[q]] : vl[q];
-                }
+            for (int q = 0; q < QG; ++q) {
+                put(q, row(ua), SC ? xget(scr, q) : vf[q]);
+                if (ub > ua) put(q, row(ub), SC ? xget(scr + 1, q) : vl[q]);
             }
         }
         __syncthreads();
