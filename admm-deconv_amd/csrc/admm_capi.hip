@@ -378,8 +378,8 @@ struct PathIn {
 //   resident 250^2           192: 2.53 vs 2.96, 128: 2.48 vs 1.99; 128^2 256: 0.88 vs 0.93, 128: 0.84 vs 0.62
 //                            -> 192 for sides >= 128 (smaller sides: every batch, the per-plane latency is small)
 //                            (sides < 128: 96^2 0.43 vs 0.40 at 1..16 planes, 64^2 and 32^2 faster at every count)
-//   resident_iso             256 planes: 250^2 5.10 vs 5.64, 120^2 1.28 vs 1.52, 64^2 0.56 vs 0.60; 128^2 x 192
-//                            1.45 vs 0.99, 250^2 x 64 4.41 vs 1.84  -> 256
+//   resident_iso             256 planes: 250^2 3.94 vs 5.78, 120^2 1.04 vs 1.53, 64^2 x 512 0.80 vs 0.96;
+//                            250^2 x 64 4.41 vs 1.84 (before its A / B row walkers)  -> 256
 enum MinPlanesFor { kMinFused, kMinFusedIso, kMinResident, kMinResidentIso };
 bool enough_planes(const PathIn& q, MinPlanesFor which) {
     const int o = opt(ADMM_OPT_MIN_PLANES);

@@ -178,6 +178,52 @@ __device__ __forceinline__ int dlast(int b) {
     return k;
 }
 
+// A wave's lanes over one line of MM pixels: GP neighbouring pixels per lane (Geo::GP), QG slices of 64 lanes.
+// LDS float offsets (x at dpos order within a pair row) of the lane's pixels and of its first pixel's left
+// neighbour; buffer byte offsets of the lane's pixels (+ the slice's immediate); stores of lanes past the line's
+// end go beyond the buffer (dropped) and LDS writes are masked.
+template <int MM>
+struct RowLanes {
+    static constexpr int GP = MM > 64 ? 2 : 1, QG = (MM + 64 * GP - 1) / (64 * GP);
+    static constexpr unsigned SL = 256 * GP;
+    int po[QG][GP], plo[QG];
+    unsigned gl, glst;
+    int lane;
+    __device__ __forceinline__ RowLanes() {
+        lane = tid() & 63;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            const int i0 = GP * (lane + 64 * q) < MM ? GP * (lane + 64 * q) : 0;
+#pragma unroll
+            for (int g = 0; g < GP; ++g) po[q][g] = 2 * dpos<MM>(i0 + g);
+            plo[q] = 2 * dpos<MM>(i0 == 0 ? MM - 1 : i0 - 1);
+        }
+        gl = 4u * GP * (unsigned)lane;
+        glst = GP * (lane + 64 * (QG - 1)) < MM ? gl : 0x80000000u;
+    }
+    __device__ __forceinline__ bool valid(int q) const { return q < QG - 1 || GP * (lane + 64 * q) < MM; }
+    template <int G>
+    __device__ __forceinline__ Vg<G> ld(rsrc_t r, int q, unsigned so) const { return Vg<G>::load(r, gl + SL * q, so); }
+    template <int G>
+    __device__ __forceinline__ void st(rsrc_t r, int q, unsigned so, const Vg<G>& v) const {
+        v.store(r, (q < QG - 1 ? gl : glst) + SL * q, so);
+    }
+    template <int G>
+    __device__ __forceinline__ Vg<G> xget(const float* Xf, int rbase, int q) const {
+        Vg<G> x;
+#pragma unroll
+        for (int g = 0; g < G; ++g) x.v[g] = Xf[rbase + po[q][g]];
+        return x;
+    }
+    template <int G>
+    __device__ __forceinline__ void put(float* Xf, int q, int rbase, const Vg<G>& v) const {
+        if (valid(q)) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) Xf[rbase + po[q][g]] = v.v[g];
+        }
+    }
+};
+
 template <bool INV>
 __device__ __forceinline__ float2 twv(const float2* __restrict__ tw, int e) {
     float2 w = tw[e];
@@ -628,29 +674,70 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
 
     if constexpr (MODE == kIsoA) {
         // ---- isotropic A phase: s_{k+1} = D x_{k+1} + u_k, u_k = s_k - f_k s_k (z = f s, ops.jl:10; first: u = 0),
-        // stored (in place: every element is read and rewritten by its own thread), and q = s1^2 + s2^2 of the
-        // pixel for the batch norm.  x of line j - 1 (channel 0, dim 2) and pixel i - 1 (channel 1, dim 1) from
-        // the staged rows (the halo pair holds lines jc0 - 2, jc0 - 1).  No forward transform: the next launch's
-        // B phase forms the spectrum from s_{k+1}.
+        // stored, and q = s1^2 + s2^2 of the pixel for the batch norm.  x of line j - 1 (channel 0, dim 2) and pixel
+        // i - 1 (channel 1, dim 1) from the staged rows (the halo pair holds lines jc0 - 2, jc0 - 1).  No forward
+        // transform: the next launch's B phase forms the spectrum from s_{k+1}.  Rows walked per wave as in the
+        // anisotropic update (GP pixels per lane, buffer loads RS_PD rows ahead in a ring that never moves); the
+        // first launch reads s_k and f_k through zero-size resources (every load 0: u = 0, bitwise the old branch).
+        // In place (s_in = s_out) is safe: a row is read RS_PD rows before its own wave rewrites it.
+        constexpr int GP = G::GP, QG = G::QG;
         constexpr unsigned MN = (unsigned)MM * NN;
+        using PV = Vg<GP>;
+        const RowLanes<MM> rl;
+        const int w = __builtin_amdgcn_readfirstlane(tid() >> 6);
+        const int ua = 2 + (w * T) / 8, ub = 1 + ((w + 1) * T) / 8;
+        const unsigned live = a.first ? 0u : MN * 4;
+        const rsrc_t rso = make_rsrc(a.so, 2 * live), rfm = make_rsrc(a.fm, live), rsn = make_rsrc(a.sn, 2 * MN * 4),
+                     rq = make_rsrc(a.q, MN * 4);
         auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
-        for (int idx = tid(); idx < T * MM; idx += kNT) {
-            const int u = 2 + idx / MM, i = idx - (u - 2) * MM;
-            const int j = jc0 + u - 2;
-            const float xc = Xf[row(u) + 2 * dpos<MM>(i)];
-            const float xp = Xf[row(u - 1) + 2 * dpos<MM>(i)];
-            const float xl = Xf[row(u) + 2 * dpos<MM>(i == 0 ? MM - 1 : i - 1)];
-            const unsigned e = (unsigned)j * MM + i;
-            float u0 = 0.0f, u1 = 0.0f;
-            if (!a.first) {
-                const float f = a.fm[e], o0 = a.so[e], o1 = a.so[MN + e];
-                u0 = o0 - f * o0;
-                u1 = o1 - f * o1;
+        struct AIn {
+            PV f, o0, o1;
+        };
+        auto aload = [&](AIn (&g)[QG], int u) {
+            const unsigned oj = 4u * (unsigned)((jc0 + u - 2) * MM);
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                g[q].f = rl.template ld<GP>(rfm, q, oj);
+                g[q].o0 = rl.template ld<GP>(rso, q, oj);
+                g[q].o1 = rl.template ld<GP>(rso, q, oj + 4 * MN);
             }
-            const float s0 = (xc - xp) + u0, s1 = (xc - xl) + u1;
-            a.sn[e] = s0;
-            a.sn[MN + e] = s1;
-            a.q[e] = s0 * s0 + s1 * s1;
+        };
+        auto astep = [&](int u, const AIn (&cur)[QG]) {
+            const unsigned oj = 4u * (unsigned)((jc0 + u - 2) * MM);
+            const int ru = row(u), rp = row(u - 1);
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                const PV xc = rl.template xget<GP>(Xf, ru, q), xp = rl.template xget<GP>(Xf, rp, q);
+                const float xl = Xf[ru + rl.plo[q]];
+                PV s0, s1, qq;
+#pragma unroll
+                for (int g = 0; g < GP; ++g) {
+                    const float f = cur[q].f.v[g], o0 = cur[q].o0.v[g], o1 = cur[q].o1.v[g];
+                    s0.v[g] = (xc.v[g] - xp.v[g]) + (o0 - f * o0);
+                    s1.v[g] = (xc.v[g] - (g == 0 ? xl : xc.v[g > 0 ? g - 1 : 0])) + (o1 - f * o1);
+                    qq.v[g] = s0.v[g] * s0.v[g] + s1.v[g] * s1.v[g];
+                }
+                rl.template st<GP>(rsn, q, oj, s0);
+                rl.template st<GP>(rsn, q, oj + 4 * MN, s1);
+                rl.template st<GP>(rq, q, oj, qq);
+            }
+        };
+        if (ub >= ua) {
+            constexpr int NS = RS_PD + 1;
+            AIn pf[NS][QG];
+#pragma unroll
+            for (int d = 0; d < RS_PD; ++d) aload(pf[d], ua + d);
+#pragma unroll 1
+            for (int u0 = ua; u0 <= ub; u0 += NS) {
+                static_for<0, NS>([&](auto id) {
+                    constexpr int d = decltype(id)::value;
+                    const int u = u0 + d;
+                    if (u <= ub) {
+                        aload(pf[(d + RS_PD) % NS], u + RS_PD);
+                        astep(u, pf[d]);
+                    }
+                });
+            }
         }
         __syncthreads();
         return;
@@ -844,16 +931,90 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
     } else if constexpr (MODE == kIsoB) {
         // isotropic B phase: v = H^T y + rho D^T w, w = z - u = f s - (s - f s) of s_k and f_k (ops.jl:10, 168), into
         // the pairs at dpos order (element of line jc0 + u, pixel i at float 2 ((u / 2) M + dpos(i)) + u % 2).
-        // D^T needs w of line j + 1 (channel 0) and of pixel i + 1 (channel 1): re-read, L1 / L2-served.
+        // D^T needs w of line j + 1 (channel 0) and of pixel i + 1 (channel 1): a wave walks its rows carrying f and
+        // channel 0's w of the row below into the next step, and takes channel 1's w of pixel i + 1 from the lane
+        // that computed it -- each w evaluated once, bitwise the values of a per-element evaluation.
+        constexpr int GP = G::GP, QG = G::QG;
         constexpr unsigned MN = (unsigned)MM * NN;
-        for (int idx = tid(); idx < T * MM; idx += kNT) {
-            const int u = idx / MM, i = idx - u * MM;
-            const int j = jc0 + u, jn = j + 1 == NN ? 0 : j + 1, ir = i + 1 == MM ? 0 : i + 1;
-            const unsigned e = (unsigned)j * MM + i, en = (unsigned)jn * MM + i, er = (unsigned)j * MM + ir;
-            auto wof = [](float f, float sv) { return f * sv - (sv - f * sv); };
-            const float w0 = wof(a.fm[e], a.so[e]), w0n = wof(a.fm[en], a.so[en]);
-            const float w1 = wof(a.fm[e], a.so[MN + e]), w1r = wof(a.fm[er], a.so[MN + er]);
-            Xf[2 * ((u >> 1) * MM + dpos<MM>(i)) + (u & 1)] = fmaf(a.rho, (w0 - w0n) + (w1 - w1r), a.hty[e]);
+        using PV = Vg<GP>;
+        const RowLanes<MM> rl;
+        const int lane = tid() & 63;
+        const int w = __builtin_amdgcn_readfirstlane(tid() >> 6);
+        const int ua = (w * T) / 8, ub = ((w + 1) * T) / 8 - 1;
+        const rsrc_t rso = make_rsrc(a.so, 2 * MN * 4), rfm = make_rsrc(a.fm, MN * 4), rh = make_rsrc(a.hty, MN * 4);
+        auto row = [&](int u) { return 2 * (u >> 1) * MM + (u & 1); };
+        auto wof = [](float f, float sv) { return f * sv - (sv - f * sv); };
+        auto off = [&](int u) {   // byte offset of line jc0 + u (periodic)
+            const int j = jc0 + u;
+            return 4u * (unsigned)((j >= NN ? j - NN : j) * MM);
+        };
+        struct BIn {
+            PV fn, s0n, s1, h;   // f and s channel 0 of line j + 1; s channel 1 and H^T y of line j
+        };
+        auto bload = [&](BIn (&g)[QG], int u) {
+            const unsigned oj = off(u), on = off(u + 1);
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                g[q].fn = rl.template ld<GP>(rfm, q, on);
+                g[q].s0n = rl.template ld<GP>(rso, q, on);
+                g[q].s1 = rl.template ld<GP>(rso, q, oj + 4 * MN);
+                g[q].h = rl.template ld<GP>(rh, q, oj);
+            }
+        };
+        PV fc[QG], w0c[QG];   // f and channel 0's w of the current line
+        auto bstep = [&](int u, const BIn (&cur)[QG]) {
+            PV w1[QG];
+#pragma unroll
+            for (int q = 0; q < QG; ++q)
+#pragma unroll
+                for (int g = 0; g < GP; ++g) w1[q].v[g] = wof(fc[q].v[g], cur[q].s1.v[g]);
+            float sh[QG];
+#pragma unroll
+            for (int q = 0; q < QG; ++q)
+                sh[q] = __int_as_float(__builtin_amdgcn_ds_bpermute(4 * ((lane + 1) & 63), __float_as_int(w1[q].v[0])));
+            const float p0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(w1[0].v[0])));
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                const float nx = q + 1 < QG ? sh[q + 1 < QG ? q + 1 : q] : p0;
+                const float wlast = GP * (lane + 64 * q) + GP == MM ? p0 : (lane == 63 ? nx : sh[q]);
+                PV v;
+#pragma unroll
+                for (int g = 0; g < GP; ++g) {
+                    const float w0n = wof(cur[q].fn.v[g], cur[q].s0n.v[g]);
+                    const float w1r = g + 1 < GP ? w1[q].v[g + 1 < GP ? g + 1 : g] : wlast;
+                    v.v[g] = fmaf(a.rho, (w0c[q].v[g] - w0n) + (w1[q].v[g] - w1r), cur[q].h.v[g]);
+                    w0c[q].v[g] = w0n;
+                }
+                fc[q] = cur[q].fn;
+                rl.put(Xf, q, row(u), v);
+            }
+        };
+        if (ub >= ua) {
+            {
+                const unsigned oj = off(ua);
+#pragma unroll
+                for (int q = 0; q < QG; ++q) {
+                    fc[q] = rl.template ld<GP>(rfm, q, oj);
+                    const PV s0 = rl.template ld<GP>(rso, q, oj);
+#pragma unroll
+                    for (int g = 0; g < GP; ++g) w0c[q].v[g] = wof(fc[q].v[g], s0.v[g]);
+                }
+            }
+            constexpr int NS = RS_PD + 1;
+            BIn pf[NS][QG];
+#pragma unroll
+            for (int d = 0; d < RS_PD; ++d) bload(pf[d], ua + d);
+#pragma unroll 1
+            for (int u0 = ua; u0 <= ub; u0 += NS) {
+                static_for<0, NS>([&](auto id) {
+                    constexpr int d = decltype(id)::value;
+                    const int u = u0 + d;
+                    if (u <= ub) {
+                        bload(pf[(d + RS_PD) % NS], u + RS_PD);
+                        bstep(u, pf[d]);
+                    }
+                });
+            }
         }
         __syncthreads();
         dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, al);
@@ -1059,12 +1220,12 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
 // 0.61 vs 1.59; profiles/r04_resident_pow2.jsonl).  Small batches are left to the 2-pass kernels by plan_paths.
 #define RS_SLOWER(X)
 
-// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster.  None at a full
-// wave of planes (profiles/r04_resident_iso.jsonl, r04_small_batch_paths.jsonl; 256 planes: 250^2 5.10 vs 5.64 ms,
-// 200^2 3.20 vs 3.41, 160^2 2.10 vs 2.27, 120^2 1.28 vs 1.52, 96^2 0.93 vs 1.17, 64^2 0.56 vs 0.60; 32^2 x 512 0.57
-// vs 0.69).  Below a wave the 2-pass kernels win (one launch per iteration with one plane per CU: 250^2 x 64 4.41
-// vs 1.84, 128^2 x 192 1.45 vs 0.99), which plan_paths' plane-count rule leaves to them.
-#define RS_ISO_SLOWER(X)
+// isotropic solve (resident_iso_kernel): shapes where the 2-pass isotropic kernels measured faster at a full wave of
+// planes (profiles/r04_resident_iso_rows.jsonl, 256 planes, A / B phases as row walkers: 250^2 3.94 vs 5.78 ms,
+// 200^2 2.70 vs 3.36, 160^2 1.78 vs 2.29, 120^2 1.04 vs 1.53, 96^2 0.81 vs 1.18, 64^2 x 512 0.80 vs 0.96, 32^2 x 512
+// 0.60 vs 0.69; but 128^2 1.27 vs 1.20 against the tuned power-of-two kernels).  Below a wave the 2-pass kernels
+// win (one launch per iteration with one plane per CU), which plan_paths' plane-count rule leaves to them.
+#define RS_ISO_SLOWER(X) X(128, 128)
 
 bool has_iso_shape(int M, int N, bool all) {
 #define X(m, n) \
