@@ -147,7 +147,34 @@ struct Rad {
         for (int q = 0; q < p; ++q) w *= r(q);
         return w;
     }
+    // offset of pass p's twiddles in the compact table: pass q holds W_{L_q}^{j m} for j < S_q, m = 1 .. R_q - 1
+    // at [j (R_q - 1) + m - 1]; LEN - 1 entries in all (sum of L_q - L_{q+1})
+    static constexpr int toff(int p) {
+        int o = 0;
+        for (int q = 0; q < p; ++q) o += st(q) > 1 ? st(q) * (r(q) - 1) : 0;
+        return o;
+    }
 };
+
+// The compact twiddle table of a LEN-point plan (Rad::toff) from the setup kernel's exp(-2 pi i n / LEN): the
+// R - 1 twiddles of a butterfly are neighbours (paired LDS reads at immediate offsets from one base) where the full
+// table put them j m LEN / L apart (one address computation and one read each)
+template <int LEN>
+__device__ __forceinline__ void fill_twiddles(float2* ct, const float2* __restrict__ full, int nthreads) {
+    using RD = Rad<LEN>;
+    for (int i = threadIdx.x; i < LEN - 1; i += nthreads) {
+        float2 w = make_float2(1.0f, 0.0f);
+        static_for<0, RD::P>([&](auto ip) {
+            constexpr int p = decltype(ip)::value;
+            constexpr int R = RD::r(p), S = RD::st(p), TS = LEN / RD::L(p), o0 = RD::toff(p), o1 = RD::toff(p + 1);
+            if (S > 1 && i >= o0 && i < o1) {
+                const int rr = i - o0, j = rr / (R - 1), m = 1 + rr - j * (R - 1);
+                w = full[j * m * TS];
+            }
+        });
+        ct[i] = w;
+    }
+}
 
 // position of natural index k after the DIF passes
 template <int LEN>
@@ -245,7 +272,7 @@ struct Acc {
 template <int LEN, int p, bool DIT, bool INV, bool FMAJ, int FS>
 __device__ __forceinline__ void ipass(int cnt, const float2* __restrict__ tw, Acc<FS> a) {
     using RD = Rad<LEN>;
-    constexpr int R = RD::r(p), L = RD::L(p), S = L / R, Q = LEN / R, TS = LEN / L;
+    constexpr int R = RD::r(p), L = RD::L(p), S = L / R, Q = LEN / R;
     const int total = cnt * Q;
     auto where = [&](int idx, int& f, int& base, int& j) {
         int b;
@@ -260,15 +287,17 @@ __device__ __forceinline__ void ipass(int cnt, const float2* __restrict__ tw, Ac
         j = b - blk * S;
         base = blk * L + j;
     };
+    // tw: the compact table (fill_twiddles): this butterfly's R - 1 twiddles are neighbours
     auto fly = [&](float2 (&v)[R], int j) {
+        const float2* tp = tw + RD::toff(p) + j * (R - 1);
         if constexpr (DIT && S > 1) {
 #pragma unroll
-            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tw, j * m * TS));
+            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tp, m - 1));
         }
         dftR<R, INV>(v);
         if constexpr (!DIT && S > 1) {
 #pragma unroll
-            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tw, j * m * TS));
+            for (int m = 1; m < R; ++m) v[m] = cmul(v[m], twv<INV>(tp, m - 1));
         }
     };
     // two butterflies in flight for small radices; one for R > 10 (register pressure next to the spectrum)
@@ -342,39 +371,16 @@ struct Geo {
             if (fits(n) && n * nr(n) <= min_regs() + 2) return n;
         return 0;
     }
-    // Register-column layout (RS_RCOL, column_chunk_rc): LS line slots with LS | NN, so that a thread's lines
-    // jt, jt + LS, .. are one decimated column of L2 = NN / LS points: an L2-point DFT in registers, a twiddle,
-    // and LS-point DFTs across the LS threads of a bin (one LDS exchange each way).  LS even (line pairs), at
-    // most 16 and at most L2 (every thread gets a k1 of the cross-thread stage); fewest registers, then
-    // fewest chunks.  0: no such LS (the shape keeps the LDS-pass column phase).
-    static constexpr bool rc_ok(int l) {
-        return l >= 2 && l % 2 == 0 && NN % l == 0 && l <= 16 && l * l <= NN && NN / l <= 32 &&
-               sm::max_prime(NN / l) <= 31 && (kNT / l) * (NN | 1) <= kBudget;
-    }
-    static constexpr int rc_regs(int l) { return cdiv(H, kNT / l) * (NN / l); }
-    static constexpr int rc_ls() {
-        int best = 0;
-        for (int l = 2; l <= 16; l += 2)
-            if (rc_ok(l) && (best == 0 || rc_regs(l) < rc_regs(best) ||
-                             (rc_regs(l) == rc_regs(best) && cdiv(H, kNT / l) < cdiv(H, kNT / best))))
-                best = l;
-        return best;
-    }
-#ifndef RS_RCOL
-#define RS_RCOL 0
-#endif
-    static constexpr int RCLS = RS_RCOL ? rc_ls() : 0;
-    static constexpr bool RC = RCLS != 0;          // register-column phase
 #ifdef RS_NCC_FORCE   // experiments: column chunk count forced
-    static constexpr int NCC = RC ? cdiv(H, kNT / RCLS) : fits(RS_NCC_FORCE) ? RS_NCC_FORCE : ncc();
+    static constexpr int NCC = fits(RS_NCC_FORCE) ? RS_NCC_FORCE : ncc();
 #else
-    static constexpr int NCC = RC ? cdiv(H, kNT / RCLS) : ncc();   // column chunks
+    static constexpr int NCC = ncc();              // column chunks
 #endif
-    static constexpr int KBC = RC ? kNT / RCLS : kbc(NCC);         // bins per column chunk
-    static constexpr int LS = RC ? RCLS : ls(NCC);                 // line slots
-    static constexpr int NR = RC ? NN / RCLS : nr(NCC);            // registers per column chunk
+    static constexpr int KBC = kbc(NCC);           // bins per column chunk
+    static constexpr int LS = ls(NCC);             // line slots
+    static constexpr int NR = nr(NCC);             // registers per column chunk
     static constexpr int NREG = NCC * NR;          // spectrum registers (float2) per thread
-    static constexpr int FS = RC ? (NN | 1) : fs(NCC);
+    static constexpr int FS = fs(NCC);
     static constexpr int QN = cdiv(MM, 64);        // pixels per lane and row in the update
     static constexpr int GP = MM > 64 ? 2 : 1;     // neighbouring pixels per lane in the row update
     static constexpr int QG = cdiv(MM, 64 * GP);   // slices of 64 lanes per row
@@ -481,86 +487,6 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, 
         for (int r = 0; r < NR; ++r) S[R0 + r] = col[r * G::LS + th.jt];
     }
     __syncthreads();
-}
-
-// ---- register column phase, chunk C (Geo::RC): the dim-2 transform of bin kc0 + kk split as NN = LS x L2 --------
-// Thread (kk, jt) holds x[jt + LS r], r < L2, of its bin (registers [C NR, C NR + NR)).  With j = jt + LS r and
-// k = k1 + L2 k2:  X[k] = sum_jt W_LS^{jt k2} W_NN^{jt k1} (sum_r x[jt + LS r] W_L2^{r k1}).
-//   1. L2-point DFT over the thread's registers, x W_NN^{jt k1} (jt k1 < NN: one table entry, no reduction);
-//   2. to LDS at slot k1 LS + jt of the bin's column; barrier;
-//   3. thread jt takes k1 = jt, jt + LS, ..: LS-point DFT over jt -> X[k1 + L2 k2], x Ct at that frequency (the
-//      C / (MN) of ops.jl:86), inverse LS-point DFT, in place; barrier;
-//   4. slot k1 LS + jt back, x conj W_NN^{jt k1}, inverse L2-point DFT -> the registers.
-// Unnormalised both ways, as the LDS-pass phase: the same arithmetic contract, two LDS round trips and three
-// barriers per chunk instead of a round trip and a barrier per radix pass.
-template <int MM, int NN, int C, int NREG>
-__device__ __forceinline__ void column_chunk_rc(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
-    using G = Geo<MM, NN>;
-    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
-    constexpr int LS = G::LS, L2 = NN / LS, NR = G::NR, R0 = C * NR, KB = G::KBC, H = G::H, FB = G::FS;
-    static_assert(NR == L2 && LS * L2 == NN, "register column layout");
-    constexpr int kc0 = C * KB, kc1 = imin(H, kc0 + KB), kc = kc1 - kc0;
-    constexpr int NK = cdiv(L2, LS);   // k1 values per thread in step 3
-    const int kk = th.kk, jt = th.jt;
-    const bool live = kk < kc;         // the thread's bin is in this chunk
-    float2 v[L2];
-#pragma unroll
-    for (int r = 0; r < L2; ++r) v[r] = S[R0 + r];
-    dftR<L2, false>(v);
-#pragma unroll
-    for (int k1 = 1; k1 < L2; ++k1) v[k1] = cmul(v[k1], twv<false>(th.twn, jt * k1));
-    // multipliers of step 3, issued before the exchange (one L2 latency per chunk): bin kc0 + kk, frequency
-    // k1 + L2 k2 at Ct[(k1 + L2 k2) H + bin]; the k2 row is a constant SGPR offset
-    const rsrc_t rc = make_rsrc(Ct, (unsigned)(H * NN * 4));
-    float cm[NK][LS];
-#pragma unroll
-    for (int m = 0; m < NK; ++m) {
-        const int k1 = imin(jt + LS * m, L2 - 1);
-        const unsigned vo = 4u * (unsigned)(k1 * H + kc0 + (live ? kk : 0));
-#pragma unroll
-        for (int k2 = 0; k2 < LS; ++k2) cm[m][k2] = bld1(rc, vo, 4u * (unsigned)(k2 * L2 * H));
-    }
-    float2* col = th.buf + kk * FB;
-    if (live) {
-#pragma unroll
-        for (int k1 = 0; k1 < L2; ++k1) col[k1 * LS + jt] = v[k1];
-    }
-    __syncthreads();
-    if (live) {
-#pragma unroll
-        for (int m = 0; m < NK; ++m) {
-            const int k1 = jt + LS * m;
-            if (m < NK - 1 || k1 < L2) {
-                float2 w[LS];
-#pragma unroll
-                for (int j = 0; j < LS; ++j) w[j] = col[k1 * LS + j];
-                dftR<LS, false>(w);
-#pragma unroll
-                for (int k2 = 0; k2 < LS; ++k2) w[k2] = cscale(w[k2], cm[m][k2]);
-                dftR<LS, true>(w);
-#pragma unroll
-                for (int j = 0; j < LS; ++j) col[k1 * LS + j] = w[j];
-            }
-        }
-    }
-    __syncthreads();
-    {   // every thread reads back every register (threads past the chunk's bins: a valid column, never used)
-        const float2* cr = th.buf + imin(kk, kc - 1) * FB;
-#pragma unroll
-        for (int k1 = 0; k1 < L2; ++k1) v[k1] = cr[k1 * LS + jt];
-    }
-#pragma unroll
-    for (int k1 = 1; k1 < L2; ++k1) v[k1] = cmul(v[k1], twv<true>(th.twn, jt * k1));
-    dftR<L2, true>(v);
-#pragma unroll
-    for (int r = 0; r < L2; ++r) S[R0 + r] = v[r];
-    __syncthreads();
-}
-
-template <int MM, int NN, int C, int NREG>
-__device__ __forceinline__ void column_phase_chunk(float2 (&S)[NREG], const Thr& th, const float* __restrict__ Ct) {
-    if constexpr (Geo<MM, NN>::RC) column_chunk_rc<MM, NN, C>(S, th, Ct);
-    else column_chunk<MM, NN, C>(S, th, Ct);
 }
 
 // ---- line phase, chunk C: lines [jc0, jc1) ---------------------------------------------------------------
@@ -1071,8 +997,8 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* twm = reinterpret_cast<float2*>(smem_raw);
     float2* twn = twm + MM;
-    for (int i = threadIdx.x; i < MM; i += kNT) twm[i] = twM[i];
-    for (int i = threadIdx.x; i < NN; i += kNT) twn[i] = twN[i];
+    fill_twiddles<MM>(twm, twM, kNT);
+    fill_twiddles<NN>(twn, twN, kNT);
     const size_t plane = blockIdx.x;
     const unsigned t = threadIdx.x;
     Thr th;
@@ -1101,7 +1027,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #pragma unroll 1
     for (int it = 1; it <= maxit; ++it) {
 #ifndef RS_SKIP_COL
-        static_for<0, G::NCC>([&](auto ic) { column_phase_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+        static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
 #endif
         if (it == maxit) {
             static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
@@ -1155,8 +1081,8 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* twm = reinterpret_cast<float2*>(smem_raw);
     float2* twn = twm + MM;
-    for (int i = threadIdx.x; i < MM; i += kNT) twm[i] = twM[i];
-    for (int i = threadIdx.x; i < NN; i += kNT) twn[i] = twN[i];
+    fill_twiddles<MM>(twm, twM, kNT);
+    fill_twiddles<NN>(twn, twN, kNT);
     const size_t plane = blockIdx.x;
     const unsigned t = threadIdx.x;
     Thr th;
@@ -1186,7 +1112,7 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
     } else {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kIsoB>(S, hs, th, la); });
     }
-    static_for<0, G::NCC>([&](auto ic) { column_phase_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+    static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
     if (k == K - 1) {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
         return;
