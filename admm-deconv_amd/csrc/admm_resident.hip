@@ -750,15 +750,21 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                 PV a0n, a1, h;
             };
             // (the first iteration reads s_old through a zero-size resource: every load returns 0, no branch)
+            // rows past the wave's last are not loaded at all (a zero-size resource, a scalar select): the ring's
+            // look-ahead would otherwise read the next wave's rows (L2 hits) and, at a chunk's end, the next
+            // chunk's (HBM again, long evicted when that chunk runs)
+            const rsrc_t rnh = make_rsrc(a.hty, 0u);
             auto gload = [&](GIn (&gi)[QG], int u) {
                 const int j = jc0 + u - 2;
                 const int jn = j + 1 == NN ? 0 : j + 1;
                 const unsigned oj = 4u * (unsigned)(j * MM), on = 4u * (unsigned)(jn * MM);
+                const bool in = u <= ub;
+                const rsrc_t rhu = in ? rh : rnh, rsu = in ? rso : rnone;
 #pragma unroll
                 for (int q = 0; q < QG; ++q) {
-                    gi[q].h = ld(rh, q, oj);
-                    gi[q].a0n = ld(rso, q, on);
-                    gi[q].a1 = ld(rso, q, oj + 4 * MN);
+                    gi[q].h = ld(rhu, q, oj);
+                    gi[q].a0n = ld(rsu, q, on);
+                    gi[q].a1 = ld(rsu, q, oj + 4 * MN);
                 }
             };
             auto step = [&](int u, const GIn (&cur)[QG]) {
