@@ -619,13 +619,15 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         struct AIn {
             PV f, o0, o1;
         };
+        const rsrc_t rnone = make_rsrc(a.sn, 0u);   // rows past the wave's last: not loaded (as in the update)
         auto aload = [&](AIn (&g)[QG], int u) {
             const unsigned oj = 4u * (unsigned)((jc0 + u - 2) * MM);
+            const rsrc_t rf = u <= ub ? rfm : rnone, rs = u <= ub ? rso : rnone;
 #pragma unroll
             for (int q = 0; q < QG; ++q) {
-                g[q].f = rl.template ld<GP>(rfm, q, oj);
-                g[q].o0 = rl.template ld<GP>(rso, q, oj);
-                g[q].o1 = rl.template ld<GP>(rso, q, oj + 4 * MN);
+                g[q].f = rl.template ld<GP>(rf, q, oj);
+                g[q].o0 = rl.template ld<GP>(rs, q, oj);
+                g[q].o1 = rl.template ld<GP>(rs, q, oj + 4 * MN);
             }
         };
         auto astep = [&](int u, const AIn (&cur)[QG]) {
@@ -883,14 +885,17 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         struct BIn {
             PV fn, s0n, s1, h;   // f and s channel 0 of line j + 1; s channel 1 and H^T y of line j
         };
+        const rsrc_t rnone = make_rsrc(a.hty, 0u);   // rows past the wave's last: not loaded (as in the update)
         auto bload = [&](BIn (&g)[QG], int u) {
             const unsigned oj = off(u), on = off(u + 1);
+            const bool in = u <= ub;
+            const rsrc_t rf = in ? rfm : rnone, rs = in ? rso : rnone, rhh = in ? rh : rnone;
 #pragma unroll
             for (int q = 0; q < QG; ++q) {
-                g[q].fn = rl.template ld<GP>(rfm, q, on);
-                g[q].s0n = rl.template ld<GP>(rso, q, on);
-                g[q].s1 = rl.template ld<GP>(rso, q, oj + 4 * MN);
-                g[q].h = rl.template ld<GP>(rh, q, oj);
+                g[q].fn = rl.template ld<GP>(rf, q, on);
+                g[q].s0n = rl.template ld<GP>(rs, q, on);
+                g[q].s1 = rl.template ld<GP>(rs, q, oj + 4 * MN);
+                g[q].h = rl.template ld<GP>(rhh, q, oj);
             }
         };
         PV fc[QG], w0c[QG];   // f and channel 0's w of the current line
