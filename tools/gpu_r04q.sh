@@ -1,4 +1,4 @@
-# round 4, seventeenth GPU call: the whole GPU suite, smoke() and the default bench line on the current build
+# round 4, seventeenth and last GPU calls: the whole GPU suite, smoke() and the default bench line on the current build
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
