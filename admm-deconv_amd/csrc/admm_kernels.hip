@@ -33,6 +33,7 @@
 namespace admm {
 
 constexpr int kThreads = 256;
+constexpr int kSetupPsfLds = 4096;   // PSF taps the setup kernel stages in LDS (larger PSFs are read from global)
 
 // XCD-aware block order (2-D grid (x, y) -> logical (x, y)).  Workgroups are dealt round-robin over
 // the 8 XCDs, each with its own L2 (MI355X_MICROARCH.md, workgroup dispatch): the bijective remap
@@ -97,6 +98,13 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
         sincospi(-2.0 * (double)t / (double)N, &s, &c);
         tN[t] = make_double2(c, s);
     }
+    // the PSF in LDS when it has at most kSetupPsfLds taps (the launch sizes the LDS for it): each bin reads every
+    // tap, and a global load per tap waited on inside the runtime-length loop cost an L2 latency per term
+    const bool psf_lds = kh * kw <= kSetupPsfLds;
+    float* hl = reinterpret_cast<float*>(tN + N);
+    if (psf_lds)
+        for (int t = threadIdx.x; t < kh * kw; t += blockDim.x) hl[t] = h[t];
+    const float* hs = psf_lds ? hl : h;
     __syncthreads();
     if (blockIdx.x == 0) {
         for (int t = threadIdx.x; t < M; t += blockDim.x) twM[t] = make_float2((float)tM[t].x, (float)tM[t].y);
@@ -113,17 +121,25 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
         double s2 = 1.0;
         if (kh > 0) {
             double re = 0.0, im = 0.0;
+            // table indices (b kj) mod N and (a k) mod M advanced by one addition and one conditional
+            // subtraction (kj < N, k < M) instead of an integer division per term: the same entries
+            int ib = 0;
             for (int b = 0; b < kw; ++b) {
-                const double2 eb = tN[(b * kj) % N];
+                const double2 eb = tN[ib];
                 double gr = 0.0, gi = 0.0;
+                int ia = 0;
                 for (int a = 0; a < kh; ++a) {
-                    const double w = (double)h[b * kh + a];
-                    const double2 ea = tM[(a * k) % M];
+                    const double w = (double)hs[b * kh + a];
+                    const double2 ea = tM[ia];
                     gr += w * ea.x;
                     gi += w * ea.y;
+                    ia += k;
+                    if (ia >= M) ia -= M;
                 }
                 re += gr * eb.x - gi * eb.y;
                 im += gr * eb.y + gi * eb.x;
+                ib += kj;
+                if (ib >= N) ib -= N;
             }
             s2 = re * re + im * im;
             if (SigT) SigT[q] = make_double2(re, im);   // top-left PSF spectrum (backward h_bar)
