@@ -43,10 +43,13 @@ using sm::SP;
 
 constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 per SIMD)
 #ifndef RS_PD
-#define RS_PD 4                           // rows of update loads in flight ahead of the row being computed
+#define RS_PD 3                           // rows of update loads in flight ahead of the row being computed (2-5 within 1-2 %, 3 best: profiles/r04v_resident_pd.txt)
 #endif
 #ifndef RS_RAD
 #define RS_RAD 16
+#endif
+#ifndef RS_PDI
+#define RS_PDI 4                          // the same for the isotropic A / B phases (3: 250^2 iso 3.78 -> 3.93 ms)
 #endif
 #ifndef RS_PINSEP
 #define RS_PINSEP 1
@@ -603,9 +606,9 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         // stored, and q = s1^2 + s2^2 of the pixel for the batch norm.  x of line j - 1 (channel 0, dim 2) and pixel
         // i - 1 (channel 1, dim 1) from the staged rows (the halo pair holds lines jc0 - 2, jc0 - 1).  No forward
         // transform: the next launch's B phase forms the spectrum from s_{k+1}.  Rows walked per wave as in the
-        // anisotropic update (GP pixels per lane, buffer loads RS_PD rows ahead in a ring that never moves); the
+        // anisotropic update (GP pixels per lane, buffer loads RS_PDI rows ahead in a ring that never moves); the
         // first launch reads s_k and f_k through zero-size resources (every load 0: u = 0, bitwise the old branch).
-        // In place (s_in = s_out) is safe: a row is read RS_PD rows before its own wave rewrites it.
+        // In place (s_in = s_out) is safe: a row is read RS_PDI rows before its own wave rewrites it.
         constexpr int GP = G::GP, QG = G::QG;
         constexpr unsigned MN = (unsigned)MM * NN;
         using PV = Vg<GP>;
@@ -651,17 +654,17 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
             }
         };
         if (ub >= ua) {
-            constexpr int NS = RS_PD + 1;
+            constexpr int NS = RS_PDI + 1;
             AIn pf[NS][QG];
 #pragma unroll
-            for (int d = 0; d < RS_PD; ++d) aload(pf[d], ua + d);
+            for (int d = 0; d < RS_PDI; ++d) aload(pf[d], ua + d);
 #pragma unroll 1
             for (int u0 = ua; u0 <= ub; u0 += NS) {
                 static_for<0, NS>([&](auto id) {
                     constexpr int d = decltype(id)::value;
                     const int u = u0 + d;
                     if (u <= ub) {
-                        aload(pf[(d + RS_PD) % NS], u + RS_PD);
+                        aload(pf[(d + RS_PDI) % NS], u + RS_PDI);
                         astep(u, pf[d]);
                     }
                 });
@@ -937,17 +940,17 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                     for (int g = 0; g < GP; ++g) w0c[q].v[g] = wof(fc[q].v[g], s0.v[g]);
                 }
             }
-            constexpr int NS = RS_PD + 1;
+            constexpr int NS = RS_PDI + 1;
             BIn pf[NS][QG];
 #pragma unroll
-            for (int d = 0; d < RS_PD; ++d) bload(pf[d], ua + d);
+            for (int d = 0; d < RS_PDI; ++d) bload(pf[d], ua + d);
 #pragma unroll 1
             for (int u0 = ua; u0 <= ub; u0 += NS) {
                 static_for<0, NS>([&](auto id) {
                     constexpr int d = decltype(id)::value;
                     const int u = u0 + d;
                     if (u <= ub) {
-                        bload(pf[(d + RS_PD) % NS], u + RS_PD);
+                        bload(pf[(d + RS_PDI) % NS], u + RS_PDI);
                         bstep(u, pf[d]);
                     }
                 });
