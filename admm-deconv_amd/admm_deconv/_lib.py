@@ -40,7 +40,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
            "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths",
-           "admm_path_name")
+           "admm_path_name", "admm_ipc_get_handle", "admm_ipc_open", "admm_ipc_close")
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
 REC_HBAR, REC_MASKS = 1, 2
@@ -150,6 +150,12 @@ def load():
     L.admm_profile_get.argtypes = [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
     L.admm_copy_async.restype = c_int
     L.admm_copy_async.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
+    L.admm_ipc_get_handle.restype = c_int
+    L.admm_ipc_get_handle.argtypes = [c_void_p, c_void_p, ctypes.POINTER(c_size_t)]
+    L.admm_ipc_open.restype = c_int
+    L.admm_ipc_open.argtypes = [c_void_p, c_int, ctypes.POINTER(c_void_p)]
+    L.admm_ipc_close.restype = c_int
+    L.admm_ipc_close.argtypes = [c_void_p, c_int]
     L.admm_query_paths.restype = c_int
     L.admm_query_paths.argtypes = [c_int] * 4 + [ctypes.c_longlong] + [c_int] * 4 + [ctypes.POINTER(c_int)] * 2
     L.admm_path_name.restype = ctypes.c_char_p
@@ -201,6 +207,30 @@ def query_paths(M, N, iso=False, kh=0, mode=MODE_FORWARD, flags=0, want_hbar=Fal
 def copy_async(dst, src, nbytes, stream):
     """admm_copy_async: hipMemcpyAsync of nbytes between device pointers on a HIP stream handle (int)."""
     check(load().admm_copy_async(dst, src, nbytes, stream))
+
+
+IPC_HANDLE_BYTES = 64
+
+
+def ipc_get_handle(ptr):
+    """admm_ipc_get_handle: (handle bytes, byte offset of ptr in its allocation)."""
+    buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+    off = ctypes.c_size_t(0)
+    check(load().admm_ipc_get_handle(ptr, buf, ctypes.byref(off)))
+    return buf.raw, off.value
+
+
+def ipc_open(handle, device):
+    """admm_ipc_open: map a peer's allocation on this process's `device`; returns its base address (int)."""
+    if len(handle) != IPC_HANDLE_BYTES:
+        raise ValueError("IPC handle must be 64 bytes")
+    p = ctypes.c_void_p(0)
+    check(load().admm_ipc_open(handle, int(device), ctypes.byref(p)))
+    return int(p.value)
+
+
+def ipc_close(ptr, device):
+    check(load().admm_ipc_close(ptr, int(device)))
 
 
 def profile_enable(on=True):

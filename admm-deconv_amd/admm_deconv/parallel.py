@@ -70,21 +70,24 @@ class ShardGather:
     runs a barrier, so the peer writes into rank dst's buffer have landed.  The receive side is double
     buffered by step parity: the returned tensor stays valid until two more steps have been issued -- on
     EVERY rank.  step() itself does not synchronise the ranks, so with engine "ipc" a peer that runs two
-    steps ahead of rank dst would overwrite the buffer rank dst is still reading.  A caller that consumes the
-    gathered batch therefore calls gathered() (collectively) after every step it consumes; a caller that
-    only streams steps (the benchmark) never reads the buffers in between.
+    steps ahead of rank dst would overwrite the buffer rank dst is still reading.  So with "ipc" step() raises
+    unless gathered() was called (collectively) after the previous step; a caller that only streams steps and
+    never reads the buffers in between (the benchmark) passes stream_only=True.
 
     engine="ipc" moves the outputs without any collective kernel: rank dst shares its receive buffer
-    once through a HIP IPC handle, and every rank copies each solved slice into its part of it with an
-    async device copy on the second stream.  The HIP runtime hands peer copies of >= ROC_P2P_SDMA_SIZE
+    once through a HIP IPC handle (admm_ipc_get_handle), every other rank maps it on its own device
+    (admm_ipc_open) and copies each solved slice into its part of it with an async device copy on the
+    second stream.  The HIP runtime hands peer copies of >= ROC_P2P_SDMA_SIZE
     to the SDMA engines, so no CU is held while the bytes cross xGMI.  An RCCL gather keeps kernel blocks
     resident for the whole transfer, and the fused solve needs every CU: one such block costs it
     ~0.8 ms per 1.2 ms (tools/contend.py).  With ipc a receive buffer is complete once
     every rank has finished its copies (what `gathered()` waits for).  If any rank cannot open the
     handles, every rank falls back to engine "rccl" (`self.engine` says which ran)."""
 
-    def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0, engine="rccl"):
+    def __init__(self, y_local, solve, *, chunks=1, group=None, dst=0, engine="rccl", stream_only=False):
         self.y = y_local
+        self.stream_only = bool(stream_only)
+        self.consumed = -1    # last step whose gathered() was called
         self.solve = solve
         self.group = group
         self.dst = dst
@@ -114,18 +117,20 @@ class ShardGather:
         self.i = 0
 
     def _ipc_setup(self, y_local):
-        """Rank dst allocates the receive buffer and shares its IPC handle; the others open it.  Returns
+        """Rank dst allocates the receive buffers and shares their IPC handles; the others map them through the
+        library (admm_ipc_open on their OWN device: no context, stream or queue on rank dst's GPU).  Returns
         whether every rank succeeded (a collective: all ranks agree)."""
-        from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
         n = y_local.shape[0]
         full = (self.world * n,) + tuple(y_local.shape[1:])
+        nbytes = y_local.element_size() * self.world * y_local.numel()
+        self.row_bytes = y_local.element_size() * (y_local.numel() // max(n, 1))
         ok = 1
-        self.recv, self.remote = None, None
+        self.recv, self.remote, self._mapped = None, None, []
         obj = [None]
         try:
             if self.rank == self.dst:
                 self.recv = [torch.empty(full, dtype=y_local.dtype, device=y_local.device) for _ in range(2)]
-                obj = [[reduce_tensor(r)[1] for r in self.recv]]
+                obj = [[(*_lib.ipc_get_handle(r.data_ptr()), nbytes) for r in self.recv]]
         except Exception:   # noqa: BLE001 -- any failure selects the RCCL path on every rank
             ok = 0
         dist.broadcast_object_list(obj, src=self.dst, group=self.group)
@@ -133,9 +138,13 @@ class ShardGather:
             if self.rank != self.dst:
                 if obj[0] is None:
                     raise RuntimeError("no handle")
-                self.remote = [rebuild_cuda_tensor(*h) for h in obj[0]]
-                if any(tuple(r.shape) != full for r in self.remote):
-                    raise RuntimeError("shape mismatch")
+                self.remote = []
+                for handle, off, size in obj[0]:
+                    if size != nbytes:
+                        raise RuntimeError("receive buffer size mismatch")
+                    base = _lib.ipc_open(handle, y_local.device.index)
+                    self._mapped.append(base)
+                    self.remote.append(base + off)
                 # one real copy through the path the steps use (peer access, engine choice): any error
                 # here selects RCCL instead of failing mid-run; the slice is overwritten by the first step
                 self.comm = torch.cuda.Stream(device=y_local.device)
@@ -148,8 +157,22 @@ class ShardGather:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
         if int(flag.item()) == 1:
             return True
+        self.close()
         self.recv, self.remote = None, None
         return False
+
+    def close(self):
+        """Unmap the peer receive buffers this rank opened (engine "ipc"); the object is unusable afterwards."""
+        for base in getattr(self, "_mapped", []):
+            try:
+                _lib.ipc_close(base, self.y.device.index)
+            except Exception:   # noqa: BLE001 -- best effort at teardown
+                pass
+        self._mapped = []
+
+    def __del__(self):
+        if getattr(self, "_mapped", None):
+            self.close()
 
     def _out(self, b):
         """Output buffer b of this rank.  With ipc, rank dst solves straight into its own part of the
@@ -168,19 +191,25 @@ class ShardGather:
         return [self.recv[b][r * n + s: r * n + s + k] for r in range(self.world)]
 
     def _push(self, remote, out, s, k):
-        """Copy this rank's solved slice [s, s + k) into its part of rank dst's IPC-opened receive buffer, on the
-        comm stream.  An explicit hipMemcpyAsync through the library (admm_copy_async), not Tensor.copy_: a
-        cross-device copy_ also synchronises with the current stream of the PEER device, which would make this
-        process create and use a queue on rank dst's GPU.  The runtime gives device-to-device copies between
-        GPUs of >= ROC_P2P_SDMA_SIZE (1 MiB default; a c3 slice is 64 MiB / chunks) to an SDMA engine."""
+        """Copy this rank's solved slice [s, s + k) into its part of rank dst's IPC-mapped receive buffer (base
+        address `remote`), on the comm stream.  An explicit hipMemcpyAsync through the library (admm_copy_async),
+        not Tensor.copy_: a cross-device copy_ also synchronises with the current stream of the PEER device, which
+        would make this process create and use a queue on rank dst's GPU.  The runtime gives device-to-device
+        copies between GPUs of >= ROC_P2P_SDMA_SIZE (1 MiB default; a c3 slice is 64 MiB / chunks) to an SDMA
+        engine."""
         n = self.y.shape[0]
-        dst = remote[self.rank * n + s: self.rank * n + s + k]
         src = out[s:s + k]
-        assert dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype and dst.shape == src.shape
+        assert src.is_contiguous()
         src.record_stream(self.comm)
-        _lib.copy_async(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size(), self.comm.cuda_stream)
+        _lib.copy_async(remote + (self.rank * n + s) * self.row_bytes, src.data_ptr(), k * self.row_bytes,
+                        self.comm.cuda_stream)
 
     def step(self):
+        if (self.engine == "ipc" and self.world > 1 and not self.stream_only and self.i >= 1
+                and self.consumed != self.i - 1):
+            raise RuntimeError("ShardGather(engine='ipc'): call gathered() (on every rank) after each step before the "
+                               "next one -- a peer running ahead would overwrite the receive buffer rank dst is "
+                               "reading; pass stream_only=True if nothing reads the gathered batches between steps")
         b = self.i & 1
         out = self._out(b)
         if self.async_comm and self.freed[b] is not None:
@@ -225,4 +254,5 @@ class ShardGather:
             torch.cuda.synchronize(self.y.device)
         if self.engine == "ipc":
             dist.barrier(group=self.group)   # every peer's copies into rank dst's buffer have completed
+        self.consumed = self.i - 1
         return None if self.recv is None else self.recv[(self.i - 1) & 1]

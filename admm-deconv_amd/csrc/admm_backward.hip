@@ -280,15 +280,14 @@ __global__ __launch_bounds__(kThreads) void hbar_corr_kernel(const float* __rest
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     for (int tap = wave; tap < ntaps; tap += nw) {
         const int b = tap / kh, a = tap - b * kh;
-        float acc = 0.0f;
+        double d = 0.0;   // fp64 per lane: TY * M / 64 products each
         for (int p = lane; p < TY * M; p += 64) {
             const int t = p / M, i = p - t * M;
             int ii = i + a - padd;   // in (-M, 2M) for kh <= M
             ii += ii < 0 ? M : 0;
             ii -= ii >= M ? M : 0;
-            acc += Vt[p] * Yt[(t + b) * M + ii];
+            d += (double)Vt[p] * Yt[(t + b) * M + ii];
         }
-        double d = acc;
         for (int off = 32; off > 0; off >>= 1) d += __shfl_down(d, off);
         if (lane == 0) out[tap] = d;
     }
@@ -359,8 +358,8 @@ __global__ __launch_bounds__(kThreads) void hbarA_kernel(const double* __restric
     }
 }
 
-// Q[q] = sum over planes of Qp[p][q] (fixed order, fp64 result)
-__global__ void reduce_planes_kernel(const float* __restrict__ Qp, double* __restrict__ Q, int planes, int n) {
+// Q[q] = sum over planes of Qp[p][q] (fixed order, fp64)
+__global__ void reduce_planes_kernel(const double* __restrict__ Qp, double* __restrict__ Q, int planes, int n) {
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
         double s = 0.0;
         for (int p = 0; p < planes; ++p) s += Qp[(size_t)p * n + q];

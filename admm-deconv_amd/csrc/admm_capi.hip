@@ -266,7 +266,7 @@ int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* s
 
 template <int MUL, bool SAVE, bool ACCQ>
 int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst, const float* C,
-                    const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, float* Qp) {
+                    const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, double* Qp) {
     const int nt = column_threads(N);
 #define X(v)                                                                                                   \
     if (N == v && nt == kThreads) {                                                                            \
@@ -290,7 +290,7 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
 // mode: 0 = x-update C, 1 = conj(Sigma_c) (H^T), 2 = Sigma_c (H), 3 = C + save spectrum, 4 = C + accumulate Q
 int launch_column(int N, int mode, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
                   const float* C, const float2* G, const float2* twN, int L, int KB, float cs,
-                  float2* vsave = nullptr, float* Qp = nullptr) {
+                  float2* vsave = nullptr, double* Qp = nullptr) {
     switch (mode) {
         case 0: return launch_column_t<0, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
         case 1: return launch_column_t<1, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
@@ -868,7 +868,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         rc = ln.run(ADMM_K_COLUMN, [&] {
             if (smc && !vsave) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 0, opt(ADMM_OPT_SMOOTH));
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB,
-                               vsave ? 4 : 0, 1.0f, vsave, (float*)nullptr);
+                               vsave ? 4 : 0, 1.0f, vsave, (double*)nullptr);
             return 0;
         });
         if (rc) return rc;
@@ -992,7 +992,7 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
         b.nblk_line = (int)(planes * gen_nb(N, T));
     }
     b.rpart = take((size_t)K * b.nblk_line * 2 * 8);
-    b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 4) : 0;
+    b.Qp = hq ? take(planes * (size_t)(M / 2 + 1) * N * 8) : 0;   // fp64 accumulators
     b.Q = hq ? take((size_t)(M / 2 + 1) * N * 8) : 0;
     b.TY = 1;   // h_bar correlation tile: the largest of 8, 4, 2, 1 lines dividing N
     for (int t = 8; t > 1; t >>= 1)
@@ -1142,7 +1142,10 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rec_forget(workspace);   // whatever was recorded there is overwritten now
     Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
     const size_t MN = (size_t)M * N;
-    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false, planes});
+    // a sharded isotropic solve plans without the plane-count rule: every shard must take the same path, since
+    // the fused and 2-pass kernels hand the reducer their sum maps in different layouts (lane-native float2 vs
+    // natural), and uneven shards can fall on either side of a threshold
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false, red ? 0 : planes});
     for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
         rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
                          maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red, pl.fwd);
@@ -1177,8 +1180,9 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
         auto it = g_rec.find(workspace);
         pflags = (h_bar != nullptr ? ADMM_REC_HBAR : 0) | (it != g_rec.end() && it->second.masks ? ADMM_REC_MASKS : 0);
     }
+    // sharded (red): no plane-count rule, so that every shard records and sweeps in one layout (forward_impl)
     const PathPlan plan = plan_paths({M, N, iso != 0, kh > 0, phases == 3 ? ADMM_MODE_BACKWARD : ADMM_MODE_RECORD, pflags,
-                                  h_bar != nullptr, rho_bar != nullptr, planes});
+                                      h_bar != nullptr, rho_bar != nullptr, red ? 0 : planes});
     const bool want_h = plan.want_h;
     const bool ln_traj = plan.ln_traj;
     const bool use_masks = plan.masks;
@@ -1265,7 +1269,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     // s_k and D x_K enter rho_bar's <D vbar, D x_k> only (fused and iso sweeps skip them without rho_bar)
     const bool want_rho = rho_bar != nullptr;
     double* rpart = reinterpret_cast<double*>(ws + bl.rpart);
-    float* Qp = want_h ? reinterpret_cast<float*>(ws + bl.Qp) : nullptr;
+    double* Qp = want_h ? reinterpret_cast<double*>(ws + bl.Qp) : nullptr;
     const size_t sstride = planes * 2 * MN;
     const size_t clds = column_lds(N, KB), flds = fwdinv_lds(M, T);
     const size_t alds = line_lds(M, T) + 8 * 16;
@@ -1331,7 +1335,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     const int ngi = iso_ngroups(planes);
     // k = 1 launches no ISO_ADJ_R: its partial rows must read as zero
     if (iso && !iso_lane) HIPCHK(hipMemsetAsync(rpart, 0, (size_t)K * bl.nblk_line * 2 * 8, s));
-    if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 4, s));
+    if (Qp) HIPCHK(hipMemsetAsync(Qp, 0, planes * (size_t)(L + 1) * N * 8, s));
     if (gen) {
         // ---- runtime-length reverse sweep (admm_generic_bwd.hip): column, line inverse -> vbar_k in
         // HBM, then the line adjoint (aniso) or ISO_ADJ_A -> ISO_ADJ_R -> ISO_ADJ_B ----
@@ -1464,7 +1468,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] {
                 hipLaunchKernelGGL(g::column_kernel, ggc, dim3(256), lcol, s, specA, specB, Ct, Gt, twN, pN, H, KB, 2, 1.0f,
-                                   (float2*)nullptr, (float*)nullptr);
+                                   (float2*)nullptr, (double*)nullptr);
             });
             if (rc) return rc;
             rc = ln.run(ADMM_K_FINAL, [&] { hipLaunchKernelGGL(g::line_inv_kernel, ggl, dim3(256), lfw, s, specB, y_bar, twM, pM, N, T); });
@@ -1993,6 +1997,50 @@ int admm_copy_async(void* dst, const void* src, size_t bytes, void* stream) {
     if (!dst || !src) return fail(ADMM_E_INVALID, "admm_copy_async: NULL pointer");
     const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_copy_async: %s", hipGetErrorString(e));
+    return ADMM_OK;
+}
+
+static_assert(sizeof(hipIpcMemHandle_t) == ADMM_IPC_HANDLE_BYTES, "hipIpcMemHandle_t size");
+
+int admm_ipc_get_handle(const void* dev_ptr, void* handle_out, size_t* offset_out) {
+    if (!dev_ptr || !handle_out || !offset_out) return fail(ADMM_E_INVALID, "admm_ipc_get_handle: NULL pointer");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    hipError_t e = hipMemGetAddressRange(&base, &size, const_cast<void*>(dev_ptr));
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_get_handle: hipMemGetAddressRange: %s", hipGetErrorString(e));
+    hipIpcMemHandle_t h;
+    e = hipIpcGetMemHandle(&h, base);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_get_handle: hipIpcGetMemHandle: %s", hipGetErrorString(e));
+    std::memcpy(handle_out, &h, sizeof(h));
+    *offset_out = static_cast<size_t>(static_cast<const char*>(dev_ptr) - static_cast<const char*>(base));
+    return ADMM_OK;
+}
+
+int admm_ipc_open(const void* handle, int device, void** dev_ptr_out) {
+    if (!handle || !dev_ptr_out) return fail(ADMM_E_INVALID, "admm_ipc_open: NULL pointer");
+    int prev = -1;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev != device) e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_open: select device %d: %s", device, hipGetErrorString(e));
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    void* p = nullptr;
+    e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (prev != device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_open: hipIpcOpenMemHandle on device %d: %s", device, hipGetErrorString(e));
+    *dev_ptr_out = p;
+    return ADMM_OK;
+}
+
+int admm_ipc_close(void* dev_ptr, int device) {
+    if (!dev_ptr) return fail(ADMM_E_INVALID, "admm_ipc_close: NULL pointer");
+    int prev = -1;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && prev != device) e = hipSetDevice(device);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_close: select device %d: %s", device, hipGetErrorString(e));
+    e = hipIpcCloseMemHandle(dev_ptr);
+    if (prev != device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_ipc_close: %s", hipGetErrorString(e));
     return ADMM_OK;
 }
 

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
                                                      const float2* __restrict__ twN, FPlan pN, int H, int KB,
                                                      int mode, float cs, float2* __restrict__ vsave = nullptr,
-                                                     float* __restrict__ Qp = nullptr) {
+                                                     double* __restrict__ Qp = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int N = pN.n;
     float2* A = reinterpret_cast<float2*>(smem_raw);
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
         if (mode & 4) vsave[pq] = v;
         if (mode & 8) {
             const float2 fv = vsave[pq];
-            Qp[pq] += v.x * fv.x + v.y * fv.y;
+            Qp[pq] += (double)v.x * fv.x + (double)v.y * fv.y;
         }
         const int mul = mode & 3;
         R[c * N + kj] = mul == 0 ? cscale(v, cs * Ct[q]) : cmul(v, mul == 1 ? Gt[q] : cconj(Gt[q]));

@@ -277,14 +277,15 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 //   MUL = 1: complex multiplier Gt = conj(Sigma_c)/(MN)   (H^T y setup)
 //   MUL = 2: conj(Gt) = Sigma_c/(MN)                       (y_bar = H vbar_sum in the backward)
 //   SAVE   : also store the forward dim-2 spectrum (before the multiply) to vsave (trajectory for h_bar)
-//   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar)
+//   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar), in fp64:
+//            K terms per bin, later scaled by C^2 in hbarA_kernel
 // ----------------------------------------------------------------------------------------------
 template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
 __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst,
                                                           const float* __restrict__ Ct,
                                                           const float2* __restrict__ Gt,
                                                           const float2* __restrict__ twN, int L, int KB, float cs,
-                                                          float2* __restrict__ vsave, float* __restrict__ Qp) {
+                                                          float2* __restrict__ vsave, double* __restrict__ Qp) {
     constexpr bool CPLX = MUL != 0;
     constexpr int FS = NN + 1;  // per-transform LDS stride (odd: conflict-free slot-major stores)
     constexpr int P = Plan<NN>::P;
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* d
             }
             if constexpr (ACCQ) {
                 const float2* vs = vsave + (size_t)plane * NN * L;
-                float* qp = Qp + (size_t)plane * NN * H;
+                double* qp = Qp + (size_t)plane * NN * H;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int kj = j + r * Q;
@@ -389,10 +390,10 @@ __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* d
                         const float2 gd = csub(gv, gm), vd = csub(vv, vm);
                         const float2 gb = make_float2(0.5f * gd.y, -0.5f * gd.x);
                         const float2 vb = make_float2(0.5f * vd.y, -0.5f * vd.x);
-                        qp[(size_t)kj * H] += ga.x * va.x + ga.y * va.y;
-                        qp[(size_t)kj * H + L] += gb.x * vb.x + gb.y * vb.y;
+                        qp[(size_t)kj * H] += (double)ga.x * va.x + (double)ga.y * va.y;
+                        qp[(size_t)kj * H + L] += (double)gb.x * vb.x + (double)gb.y * vb.y;
                     } else {
-                        qp[(size_t)kj * H + s] += gv.x * vv.x + gv.y * vv.y;
+                        qp[(size_t)kj * H + s] += (double)gv.x * vv.x + (double)gv.y * vv.y;
                     }
                 }
             }

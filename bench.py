@@ -80,10 +80,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the config's; c3 -> 2048/N)")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the gather to rank 0 (solve only)")
     ap.add_argument("--chunks", type=int, default=1, help="N > 1: slices per shard, each gathered as soon as solved")
-    ap.add_argument("--gather-engine", default="ipc", choices=("ipc", "rccl"),
+    ap.add_argument("--gather-engine", default="both", choices=("both", "ipc", "rccl"),
                     help="N > 1: 'ipc' = every rank copies its solved slices into rank 0's IPC-shared receive buffer "
                          "(async peer copies, SDMA: no CU held); 'rccl' = dist.gather over RCCL (falls back to it "
-                         "when the IPC handle cannot be opened)")
+                         "when the IPC handle cannot be opened); 'both' (default) = the metric with ipc, plus the "
+                         "same steps with rccl timed in the same invocation (per-rank diagnostics)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: nccl (RCCL over xGMI); gloo only to rehearse the schedule with ranks sharing a GPU")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -391,7 +392,9 @@ def main():
         i = chunk_of.setdefault(ys.data_ptr(), len(chunk_of) % len(ws))
         admm_deconv.tvd_fft(ys, synth.LAMBDA, synth.RHO, h, False, K, out=xs, workspace=ws[i], stream=stream)
 
-    sg = parallel.ShardGather(y, solve, chunks=args.chunks, engine=args.gather_engine) if gather else None
+    engine = "ipc" if args.gather_engine == "both" else args.gather_engine
+    # stream_only: nothing reads the gathered batches between steps (ShardGather's ipc rule)
+    sg = parallel.ShardGather(y, solve, chunks=args.chunks, engine=engine, stream_only=True) if gather else None
 
     def step():
         if sg is not None:
@@ -399,7 +402,7 @@ def main():
         else:
             solve(y, out)
 
-    def timed(body, steps):
+    def timed(body, steps, sg=sg):
         """Barrier + synchronize on both sides of `steps` calls of body; (this rank's seconds, max over ranks,
         ms from this rank's last solve being enqueued to the end of its device work)."""
         torch.cuda.synchronize(dev)
@@ -440,6 +443,19 @@ def main():
         # gather) in this invocation, and per rank what it saw -- which engine ran, how long its own steps took,
         # how long its gathers ran past its last solve, and which device it drove
         so_rank, so_el, _ = timed(lambda: solve(y, out), args.steps) if gather else (el_rank, el, 0.0)
+        # the other gather engine on the same shards and steps (--gather-engine both): the first multi-GPU
+        # record then compares the IPC push with the RCCL gather
+        alt = None
+        if gather and args.gather_engine == "both":
+            other = "rccl" if sg.engine == "ipc" else "ipc"
+            sg2 = parallel.ShardGather(y, solve, chunks=args.chunks, engine=other, stream_only=True)
+            for _ in range(args.warmup):
+                sg2.step()
+            a_rank, a_el, a_tail = timed(sg2.step, args.steps, sg=sg2)
+            alt = {"engine": sg2.engine, "ms_per_step": round(1000.0 * a_rank / args.steps, 4),
+                   "max_ms_per_step": round(1000.0 * a_el / args.steps, 4), "value": round(images / a_el, 2),
+                   "gather_tail_ms": round(a_tail, 4)}
+            sg2.close()
         props = torch.cuda.get_device_properties(dev)
         me = {"rank": rank, "world_seen": dist.get_world_size(), "backend": dist.get_backend(),
               "device": dev.index, "visible_devices": torch.cuda.device_count(),
@@ -447,12 +463,17 @@ def main():
               "gather_engine": (sg.engine if sg is not None else None),
               "ms_per_step": round(1000.0 * el_rank / args.steps, 4),
               "solve_only_ms_per_step": round(1000.0 * so_rank / args.steps, 4),
-              "gather_tail_ms": round(tail_ms, 4)}
+              "gather_tail_ms": round(tail_ms, 4),
+              "other_engine": alt}
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
         solve_only = {"ms_per_step": round(1000.0 * so_el / args.steps, 4),
                       "value": round(images / so_el, 2),
                       "note": "same steps and shards without the gather, max over ranks (not the metric)"}
+        if alt is not None:
+            solve_only["other_engine"] = {"engine": alt["engine"], "ms_per_step": alt["max_ms_per_step"],
+                                          "value": alt["value"],
+                                          "note": "same steps gathered by the other engine, max over ranks (not the metric)"}
 
     # ---- per-kernel timing (separate instrumented solve; not part of the timed region) ----
     _lib.profile_reset()

@@ -114,7 +114,9 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
  * shard's: y_bar for its planes, and its CONTRIBUTION to h_bar / lambda_bar / rho_bar (sum them over
  * shards, as data-parallel training all-reduces every parameter gradient).
  * With iso == 0 the reducer is ignored (planes are independent).  reducer == NULL (or fn == NULL)
- * is the unsharded call, identical to admm_tvd_forward_f32 / admm_tvd_backward_f32. */
+ * is the unsharded call, identical to admm_tvd_forward_f32 / admm_tvd_backward_f32.  A sharded
+ * isotropic call ignores the plane-count rule (ADMM_OPT_MIN_PLANES): every shard takes the per-plane
+ * kernels whatever its own size, so that all shards hand the reducer their maps in one layout. */
 typedef int (*admm_reduce_fn)(float* buf, size_t count, void* stream, void* user);
 typedef struct {
     admm_reduce_fn fn;
@@ -290,6 +292,18 @@ const char* admm_path_name(int path);
  * least ROC_P2P_SDMA_SIZE (1 MiB by default) to an SDMA engine, so the transfer holds no CU and touches
  * no HIP stream of the peer device.  ADMM_E_INVALID for NULL pointers, ADMM_E_HIP if the runtime refuses. */
 int admm_copy_async(void* dst, const void* src, size_t bytes, void* stream);
+
+/* The receive buffer of that transport, shared once per run through a HIP IPC handle (no counterpart in
+ * the reference).  admm_ipc_get_handle: the ADMM_IPC_HANDLE_BYTES-byte handle of the device allocation
+ * that holds dev_ptr (a caching allocator's block may sit inside a larger allocation) and dev_ptr's byte
+ * offset in it.  admm_ipc_open: maps a peer process's handle into THIS process on `device` (the caller's
+ * own GPU; the current device is restored) with lazy peer access, *dev_ptr_out = the allocation's base
+ * (add the offset).  No context, stream or queue is created on the peer's GPU.  admm_ipc_close unmaps it.
+ * ADMM_E_INVALID for NULL pointers, ADMM_E_HIP if the runtime refuses. */
+#define ADMM_IPC_HANDLE_BYTES 64
+int admm_ipc_get_handle(const void* dev_ptr, void* handle_out, size_t* offset_out);
+int admm_ipc_open(const void* handle, int device, void** dev_ptr_out);
+int admm_ipc_close(void* dev_ptr, int device);
 
 /* Optional per-kernel timing (measurement only; off by default).  When enabled, each launch
  * inside admm_tvd_forward_f32 is bracketed by hipEvents on `stream` and the call synchronises

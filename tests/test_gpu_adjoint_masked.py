@@ -234,11 +234,12 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
 
 def check(cid, err, ref32):
     """<= 1e-5, or -- where the arithmetic itself is ill-conditioned (rho_bar's cancelling terms; the BT
-    factor's tau / |s|^3 just above the threshold) -- no worse than 3x an fp32 evaluation of the SAME
+    factor's tau / |s|^3 just above the threshold) -- no worse than the reference's own algorithm in fp32: the
+    float32 autograd of the unrolled solve (what Zygote runs for the reference, src/train.jl:51) on the SAME
     mask-conditioned computation."""
     for k in ("x", "y_bar", "lambda_bar", "rho_bar", "h_bar"):
         if k in err:
-            bound = max(TOL, 3 * ref32.get(k, 0.0))
+            bound = max(TOL, ref32.get(k, 0.0))
             assert err[k] <= bound, f"{cid}: {k} error {err[k]:.3e} > {bound:.3e} (gpu {err}, fp32 {ref32})"
 
 

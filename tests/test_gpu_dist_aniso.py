@@ -65,6 +65,7 @@ def _work(rank, world, port, q, case, n_local, chunks, engine, distinct):
 
     sg = parallel.ShardGather(yt, solve, chunks=chunks, engine=engine)
     sg.step()
+    sg.gathered()         # with ipc, required before the next step (a peer must not run two steps ahead)
     sg.step()
     got = sg.gathered()   # collective: waits for every rank's device work (and, for ipc, a barrier)
     local = sg.local()
@@ -154,6 +155,111 @@ def test_bench_two_ranks_gloo(dev):
         assert r["ms_per_step"] > 0 and r["solve_only_ms_per_step"] > 0 and r["gather_tail_ms"] >= 0
         assert r["device"] == 0 and r["visible_devices"] >= 1
     assert d["solve_only"]["value"] > 0 and d["solve_only"]["ms_per_step"] > 0
+    # --gather-engine both (default): the same steps gathered by RCCL (here gloo), timed per rank
+    for r in d["ranks"]:
+        assert r["other_engine"]["engine"] == "rccl" and r["other_engine"]["ms_per_step"] > 0
+    assert d["solve_only"]["other_engine"]["engine"] == "rccl" and d["solve_only"]["other_engine"]["value"] > 0
+
+
+def _ipc_worker(rank, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        from admm_deconv import _lib
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        # rank 0: a buffer inside a larger allocation (offset != 0, as a caching allocator hands out)
+        big = torch.zeros(3 << 20, dtype=torch.float32, device=dev)
+        view = big[(1 << 20) + 64: (2 << 20) + 64]
+        obj = [None]
+        if rank == 0:
+            view.copy_(torch.arange(1 << 20, dtype=torch.float32, device=dev))
+            torch.cuda.synchronize()
+            obj = [_lib.ipc_get_handle(view.data_ptr())]
+            assert obj[0][1] >= ((1 << 20) + 64) * 4     # the view's offset in its allocation
+        dist.broadcast_object_list(obj, src=0)
+        ok = True
+        if rank == 1:
+            handle, off = obj[0]
+            base = _lib.ipc_open(handle, dev.index)
+            local = torch.empty(1 << 20, dtype=torch.float32, device=dev)
+            st = torch.cuda.Stream(device=dev)
+            _lib.copy_async(local.data_ptr(), base + off, local.numel() * 4, st.cuda_stream)   # peer -> local
+            st.synchronize()
+            ok = bool(torch.equal(local, torch.arange(1 << 20, dtype=torch.float32, device=dev)))
+            local.fill_(-1.0)
+            _lib.copy_async(base + off, local.data_ptr(), 4096 * 4, st.cuda_stream)           # local -> peer
+            st.synchronize()
+            _lib.ipc_close(base, dev.index)
+        dist.barrier()
+        if rank == 0:
+            torch.cuda.synchronize()
+            ok = bool((view[:4096] == -1.0).all()) and bool(view[4096] == 4096.0) and bool((big[:1 << 20] == 0).all())
+        q.put((rank, ok))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_ipc_handle_open_close_through_the_library(dev):
+    """admm_ipc_get_handle / admm_ipc_open / admm_ipc_close (include/admm_deconv.h): rank 0 shares a buffer that
+    sits at an offset inside a larger allocation; rank 1 maps it on its own device, reads it and writes into it
+    with admm_copy_async, and unmaps it.  Both directions land where the offset says."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True for r in res), res
+
+
+def _ahead_worker(rank, port, q, stream_only):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        y = torch.ones(2, 1, 64, 64, device=dev)
+        sg = parallel.ShardGather(y, lambda ys, xs: xs.copy_(ys), engine="ipc", stream_only=stream_only)
+        assert sg.engine == "ipc"
+        sg.step()
+        try:
+            sg.step()
+            raised = False
+        except RuntimeError:
+            raised = True
+        sg.gathered()
+        q.put((rank, raised))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("stream_only", [False, True])
+def test_ipc_step_requires_gathered_unless_stream_only(dev, stream_only):
+    """with the ipc engine a peer two steps ahead of rank dst would overwrite the receive buffer dst
+    is reading, so step() raises unless gathered() followed the previous step -- except for stream_only
+    callers (the benchmark), which never read the buffers between steps."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ahead_worker, args=(r, port, q, stream_only)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is (not stream_only) for r in res), res
 
 
 def test_copy_async_is_a_stream_ordered_device_copy(dev):

@@ -5,7 +5,7 @@ import torch
 
 import oracle_np
 from admm_deconv import layers, synth
-from parity import assert_parity
+from parity import assert_parity, assert_parity_fp32ref
 
 pytestmark = pytest.mark.gpu
 
@@ -50,26 +50,19 @@ def test_layer_forward(dev, kind):
         # activations clip; compare with an absolute guard scaled by the pre-activation magnitude
         assert np.abs(got - ref).max() <= 2e-4 * max(1.0, np.abs(ref).max())
     else:
-        # F3 solves with a glorot-initialised 15 x 15 PSF (clamped to [0, 1]): ill-conditioned in fp32 -- an fp32
-        # torch evaluation of the same solve is 0.7e-5 .. 1.0e-5 off the fp64 oracle per plane -- so the bound is
-        # max(1e-5, 3 x that fp32 error), the rule of tests/test_gpu_adjoint_masked.py
-        e32 = fp32_solve_error(L, y)
-        assert_parity(got, ref, rel_tol=max(1e-5, 3 * e32), what=f"{kind} (fp32 evaluation {e32:.2e})")
-
-
-def fp32_solve_error(layer, y):
-    """Worst per-plane relative L2 of an fp32 torch evaluation of the layer's solve against the fp64 oracle."""
-    import oracle_torch
-    w = layer.weight.detach().cpu().numpy()
-    w = None if w.size == 0 else w.reshape(w.shape[-2:]).astype(np.float32)
-    lam, rho = np.float32(layer.lam.item()), np.float32(layer.rho.item())
-    ref = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), lam, rho,
-                                                    None if w is None else oracle_np.psf_from_c(w), layer.iso,
-                                                    layer.iters))
-    x32 = oracle_torch.tvd_fft_torch(torch.from_numpy(y), torch.tensor(lam), torch.tensor(rho),
-                                     None if w is None else torch.from_numpy(w), layer.iso, layer.iters).numpy()
-    B, P = y.shape[:2]
-    return max(np.linalg.norm(x32[b, p] - ref[b, p]) / np.linalg.norm(ref[b, p]) for b in range(B) for p in range(P))
+        # F3 solves with a glorot-initialised 15 x 15 PSF (clamped to [0, 1]) whose spectrum has near-zeros: the
+        # spectral division amplifies rounding, and every fp32 solve lands about 1e-5 from the fp64 oracle (the C
+        # fp32 reference solve 1.2e-5, fp32 torch 0.7e-5 .. 1.0e-5 per plane).  The resident 64^2 path's 1.04e-5
+        #  and the 2-pass path's lower figure are two samples of that rounding (different FFT plans
+        # and summation orders), not a defect of either.  Bound: max(1e-5, the C fp32 reference's error)
+        w = L.weight.detach().cpu().numpy()
+        w = None if w.size == 0 else w.reshape(w.shape[-2:]).astype(np.float32)
+        lam, rho = np.float32(L.lam.item()), np.float32(L.rho.item())
+        sol = oracle_np.to_c(oracle_np.tvd_fft_spectral(oracle_np.from_c(y.astype(np.float64)), lam, rho,
+                                                        None if w is None else oracle_np.psf_from_c(w), L.iso, L.iters))
+        bias = 0.0 if L.bias is False else float(L.bias.reshape(-1)[0])   # the solve before `.+ bias` (:222)
+        assert_parity(got, ref, rel_tol=1.0, maxabs_tol=1.0)                 # shape / finiteness of the layer output
+        assert_parity_fp32ref(got - np.float32(bias), sol, y, lam, rho, w, L.iso, L.iters, what=kind)
 
 
 def test_trainable_sets():

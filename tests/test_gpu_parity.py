@@ -9,7 +9,7 @@ import torch
 import admm_deconv
 import oracle_np
 from admm_deconv import synth
-from parity import assert_parity, oracle_solve
+from parity import assert_parity, assert_parity_fp32ref, c_fp32_error, oracle_solve
 
 pytestmark = pytest.mark.gpu
 
@@ -206,25 +206,15 @@ def test_c4_full_config_vs_oracle(dev):
 
 def test_demo_shape_dense_prox(dev):
     """The reference demo shape (32 x 32 PSF on 32 x 32 crops, K = 50, src/ADMM_Deconv.jl:17-23) with the prox live
-    in 59 % of the elements (lambda 0.0002, rho 0.3).  The solve is ill-conditioned in fp32 here: an fp32 torch
-    evaluation of the SAME computation, with its prox held at the fp64 oracle's own branches (so only arithmetic
-    separates the two), is 8.5e-5 off the oracle.  Bound: max(1e-5, 3 x that fp32 error), the rule
-    test_gpu_adjoint_masked.py applies to every ill-conditioned quantity.  (Measured: the GPU is at 1.7e-5.)"""
-    import oracle_torch
+    in 59 % of the elements (lambda 0.0002, rho 0.3).  The solve is ill-conditioned in fp32 here: the reference's
+    own algorithm in float32 (oracle/admm_oracle.c) is 5.9e-5 off the fp64 oracle.  Bound: max(1e-5, that error)
+    (tests/parity.py assert_parity_fp32ref).  (Measured: the GPU is at 1.7e-5.)"""
     B, P, N, M, K, lam, rho = 2, 3, 32, 32, 50, 0.0002, 0.3
     rng = np.random.default_rng(B * 1000 + N + M + K)
     h = make_psf(("rand", 32, 32), rng)
     y = synth.make_batch(B, M, N, h, P=P, g0=7)
     got = run_gpu(dev, y, lam, rho, h, False, K)
     ref = run_oracle(y, lam, rho, h, False, K, what="demo dense prox")
-    rec = []
-    l64, r64 = (torch.tensor(float(np.float32(v)), dtype=torch.float64) for v in (lam, rho))
-    oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)), l64, r64, torch.from_numpy(h.astype(np.float64)),
-                               False, K, record=rec)
-    masks = oracle_torch.masks_from_trajectory(np.stack([r[0].numpy() for r in rec]), lam, rho, False, None)
-    x32 = oracle_torch.tvd_fft_torch(torch.from_numpy(y), torch.tensor(np.float32(lam)), torch.tensor(np.float32(rho)),
-                                     torch.from_numpy(h), False, K, masks=masks).numpy()
-    e32 = max(np.linalg.norm(x32[b, p] - ref[b, p]) / np.linalg.norm(ref[b, p]) for b in range(B) for p in range(P))
-    bound = max(1e-5, 3 * e32)
-    worst, _ = assert_parity(got, ref, rel_tol=bound, what=f"demo dense prox (fp32 evaluation {e32:.2e})")
+    e32, _ = c_fp32_error(y, lam, rho, h, False, K, ref)
     assert e32 > 1e-5, "the case is meant to be ill-conditioned in fp32"
+    assert_parity_fp32ref(got, ref, y, lam, rho, h, False, K, what="demo dense prox")

@@ -12,7 +12,7 @@ import torch
 import admm_deconv
 import oracle_np
 from admm_deconv import _lib, synth
-from parity import assert_parity, oracle_solve
+from parity import assert_parity_fp32ref, assert_parity, oracle_solve
 
 pytestmark = pytest.mark.gpu
 
@@ -122,9 +122,11 @@ ISO_CASES = [
     (3, 1, 250, 250, ("gauss", 15, 2.5), 0.0041, 0.021, 25),
     (2, 3, 128, 128, None, 0.0041, 0.021, 20),                 # the c5 denoiser layer at 128 x 128
     (4, 1, 96, 96, ("rand", 7, 5), 0.02, 0.1, 8),
-    # the reference demo shape, isotropic: lambda 0.0008 puts the BT prox live in 21 % of the pairs while an
-    # fp32 evaluation stays 1.6e-6 off the oracle (0.00035: 99.97 % live, but fp32 itself is 4.7e-5 off)
+    # the reference demo shape, isotropic: lambda 0.0008 puts the BT prox live in 21 % of the pairs (the C fp32
+    # reference solve 2.5e-6 off the oracle); 0.00035 in 99.97 %, ill-conditioned: the C fp32 reference solve
+    # is 4.7e-5 off, the bound of assert_parity_fp32ref (round 4 measured the GPU at 1.4e-5 there)
     (2, 3, 32, 32, ("rand", 32, 32), 0.0008, 0.3, 30),
+    (2, 3, 32, 32, ("rand", 32, 32), 0.00035, 0.3, 30),
     (5, 1, 200, 200, ("gauss", 9, 1.5), 0.01, 0.05, 1),         # K = 1: the first launch is the last
     (2, 1, 160, 160, ("gauss", 9, 1.5), 0.01, 0.05, 2),
 ]
@@ -149,9 +151,12 @@ def test_resident_iso_parity_vs_oracle_and_2pass(dev, case):
     got = _solve_iso(dev, y, lam, rho, h, K, True)
     two = _solve_iso(dev, y, lam, rho, h, K, False)
     ref = oracle_solve(y, lam, rho, h, True, K, "spectral", linear_only=K == 1, what="resident iso " + str(case))
-    assert_parity(got, ref, what="resident iso " + str(case))
+    e_res = assert_parity_fp32ref(got, ref, y, lam, rho, h, True, K, what="resident iso " + str(case))[2]
+    e_two = assert_parity_fp32ref(two, ref, y, lam, rho, h, True, K, what="2-pass iso " + str(case))[2]
     d = np.linalg.norm((got - two).ravel()) / np.linalg.norm(two.ravel())
-    assert d < 1e-5, f"resident iso vs 2-pass rel-L2 {d:.2e}"
+    # two fp32 solves within the bound of the oracle are within twice it of each other
+    bound = 1e-5 if e_res is None and e_two is None else 2 * max(e_res or 0.0, e_two or 0.0, 1e-5)
+    assert d < bound, f"resident iso vs 2-pass rel-L2 {d:.2e} > {bound:.1e}"
 
 
 def test_resident_iso_deterministic_and_couples_batch(dev):
