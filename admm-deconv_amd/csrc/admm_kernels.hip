@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "fft_reg.hpp"
+#include "scalar_src.hpp"
 
 namespace admm {
 
@@ -64,12 +65,6 @@ __device__ __forceinline__ XBlk xcd_block() {
 // or, when a pointer is NULL, the host value.  setup_kernel resolves them once into the
 // workspace's scalar block prm = {tau = lambda / rho (fp32, ops.jl:20), rho, lambda}; every later
 // kernel of the solve reads prm, and a recording's replay reuses the block the recording resolved.
-struct ScalarSrc {
-    const float* lam;
-    const float* rho;
-    float lam_v;
-    float rho_v;
-};
 __device__ __forceinline__ float src_lam(const ScalarSrc& sc) { return sc.lam ? *sc.lam : sc.lam_v; }
 __device__ __forceinline__ float src_rho(const ScalarSrc& sc) { return sc.rho ? *sc.rho : sc.rho_v; }
 __device__ __forceinline__ void write_prm(const ScalarSrc& sc, float* prm) {

@@ -115,8 +115,27 @@ def pad_asm(text):
     return "\n".join(out), inserted
 
 
-def compile_tu(src, obj, flags, verbose=False):
-    """hipcc -c `src` -> `obj` with `flags`, the device assembly padded by pad_asm.  Returns the s_nop count."""
+KERNEL = re.compile(r"^\s*\.amdhsa_kernel\s+(\S+)")
+SCRATCH = re.compile(r"^\s*\.amdhsa_private_segment_fixed_size\s+(\d+)")
+
+
+def scratch_sizes(text):
+    """{kernel symbol: private (scratch) segment bytes per lane} from the kernel descriptors of device assembly."""
+    out, cur = {}, None
+    for line in text.split("\n"):
+        m = KERNEL.match(line)
+        if m:
+            cur = m.group(1)
+            continue
+        m = SCRATCH.match(line)
+        if m and cur is not None:
+            out[cur] = int(m.group(1))
+    return out
+
+
+def compile_tu(src, obj, flags, verbose=False, scratch_out=None):
+    """hipcc -c `src` -> `obj` with `flags`, the device assembly padded by pad_asm.  Returns the s_nop count;
+    `scratch_out` (a dict), when given, receives every kernel's scratch bytes per lane (scratch_sizes)."""
     work = obj + ".hz"
     shutil.rmtree(work, ignore_errors=True)
     os.makedirs(work)
@@ -134,6 +153,8 @@ def compile_tu(src, obj, flags, verbose=False):
                 raise RuntimeError(f"cannot find the device assembly in: {step[:200]}")
             path = os.path.join(work, m.group(1))
             text, n = pad_asm(open(path).read())
+            if scratch_out is not None:
+                scratch_out.update(scratch_sizes(text))
             open(path, "w").write(text)
             total += n
         rr = subprocess.run(step, shell=True, cwd=work, capture_output=True, text=True)

@@ -42,7 +42,8 @@ def _make_C(M, N, rho, h):
     return 1.0 / (s2 + rho * lap)
 
 
-def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, record=None, tau=None, terms=None):
+def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, record=None, tau=None, terms=None,
+                  h_C=None):
     """y: (B,P,N,M) float64 tensor; lam, rho: 0-d tensors; h: (kw,kh) tensor or None.  Returns x.
 
     masks (optional): the prox's branch decisions held fixed, one entry per iteration k = 1..maxit-1 --
@@ -59,7 +60,9 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
     terms (optional dict): every use of rho and tau gets its own elementwise copy (lists terms["rho"],
     terms["tau"]; retain_grad), so that after backward() the sum of |grad| over them is the sum of the
     absolute values of the terms rho_bar and tau_bar add up -- the scale fp summation error is measured
-    against (the gradients are heavily cancelling sums)."""
+    against (the gradients are heavily cancelling sums).
+    h_C (optional): the PSF as it enters C = 1/(|Sigma|^2 + rho |Lambda|^2) (ops.jl:22-37), a separate leaf from
+    the `h` of H^T y (ops.jl:71-81), so that h_bar splits into its two paths (tvd_fft_grads_split)."""
     B, P, N, M = y.shape
     if tau is None:
         tau = lam / rho                                               # ops.jl:20
@@ -72,7 +75,8 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
         c.retain_grad()
         terms.setdefault(kind, []).append(c)
         return c
-    C = _make_C(M, N, rho, h)
+    hc = h if h_C is None else h_C
+    C = _make_C(M, N, rho, hc)
     hty = y if h is None else _ht(y, h)
     x = torch.zeros_like(y)
     z1 = torch.zeros_like(y); z2 = torch.zeros_like(y)
@@ -81,7 +85,7 @@ def tvd_fft_torch(y, lam, rho, h=None, isotropic=False, maxit=100, masks=None, r
         w1, w2 = z1 - u1, z2 - u2
         dtw = (w1 - torch.roll(w1, -1, dims=-2)) + (w2 - torch.roll(w2, -1, dims=-1))
         if terms is not None:
-            C = _make_C(M, N, _own(rho0, (N, M // 2 + 1), "rho"), h)
+            C = _make_C(M, N, _own(rho0, (N, M // 2 + 1), "rho"), hc)
             rho = _own(rho0, y.shape, "rho")
         x = torch.fft.irfft2(C * torch.fft.rfft2(hty + rho * dtw), s=(N, M))
         d1 = x - torch.roll(x, 1, dims=-2)                             # x[i,j]-x[i,j-1]
@@ -146,7 +150,9 @@ def tvd_fft_grads_split(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64, m
     """Gradients with tau = lam / rho as its own variable: returns (x, ybar, hbar, tau_bar, rho_bar_explicit).
     Then lam_bar = tau_bar / rho and rho_bar = rho_bar_explicit - tau_bar lam / rho^2.
     scales (optional dict): receives "tau" = sum of |terms| of tau_bar and "rho" = of rho_bar_explicit (see
-    tvd_fft_torch `terms`): the condition scales of the two cancelling sums."""
+    tvd_fft_torch `terms`): the condition scales of the two cancelling sums; and, with a PSF, "h" = per tap
+    |h_bar through H^T y| + |h_bar through C| (the two paths cancel: |h_bar| is ~1/2.7 of that at the c2 and
+    128^2 test shapes)."""
     y = torch.as_tensor(y, dtype=dtype).clone().requires_grad_(True)
     lam_v = float(lam)
     rho_t = torch.tensor(float(rho), dtype=dtype, requires_grad=True)
@@ -155,10 +161,16 @@ def tvd_fft_grads_split(y, lam, rho, h, iso, maxit, xbar, dtype=torch.float64, m
     if h is not None and h.size:
         h_t = torch.as_tensor(h, dtype=dtype).clone().requires_grad_(True)
     terms = {} if scales is not None else None
-    x = tvd_fft_torch(y, torch.tensor(lam_v, dtype=dtype), rho_t, h_t, iso, maxit, masks, tau=tau_t, terms=terms)
+    h_c = None if (h_t is None or scales is None) else h_t.detach().clone().requires_grad_(True)
+    x = tvd_fft_torch(y, torch.tensor(lam_v, dtype=dtype), rho_t, h_t, iso, maxit, masks, tau=tau_t, terms=terms,
+                      h_C=h_c)
     (x * torch.as_tensor(xbar, dtype=dtype)).sum().backward()
+    hbar = None if h_t is None else h_t.grad.numpy()
     if scales is not None:
         for k in ("tau", "rho"):
             scales[k] = float(sum(t.grad.abs().sum() for t in terms.get(k, []) if t.grad is not None))
+        if h_c is not None:
+            scales["h"] = h_t.grad.abs().numpy() + h_c.grad.abs().numpy()
+            hbar = hbar + h_c.grad.numpy()
     g = lambda t: float(t.grad) if t.grad is not None else 0.0  # noqa: E731
-    return (x.detach().numpy(), y.grad.numpy(), None if h_t is None else h_t.grad.numpy(), g(tau_t), g(rho_t))
+    return (x.detach().numpy(), y.grad.numpy(), hbar, g(tau_t), g(rho_t))

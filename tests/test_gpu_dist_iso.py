@@ -126,6 +126,17 @@ def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
                                                         torch.from_numpy(xbar).to(dev), LAM, RHO, ht, True, K,
                                                         need_h=need_rho, need_rho=need_rho)
     yb0, lb0 = yb0.cpu().numpy(), float(lb0)
+    # the spread of the scalar gradients under a reordered batch sum: the same single-process solve with the
+    # batch in other plane orders (mathematically identical: pixelnorm and every gradient sum over the planes)
+    spread = {"lam": 0.0, "rho": 0.0, "h": 0.0}
+    for order in (np.arange(nb)[::-1], np.r_[np.arange(0, nb, 2), np.arange(1, nb, 2)]):
+        _, _, hbp, lbp, rbp = admm_deconv.tvd_fft_backward(
+            torch.from_numpy(np.ascontiguousarray(y[order])).to(dev), torch.from_numpy(np.ascontiguousarray(xbar[order])).to(dev),
+            LAM, RHO, ht, True, K, need_h=need_rho, need_rho=need_rho)
+        spread["lam"] = max(spread["lam"], abs(float(lbp) - lb0))
+        if need_rho:
+            spread["rho"] = max(spread["rho"], abs(float(rbp) - float(rb0)))
+            spread["h"] = max(spread["h"], float(np.linalg.norm(hbp.cpu().numpy() - hb0.cpu().numpy())))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -141,9 +152,14 @@ def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
     assert _rel(x, x0) < 1e-5
     assert _rel(np.concatenate([r[2] for r in res]), x0) < 1e-5
     _check_y_bar(np.concatenate([r[3] for r in res]), yb0)
-    assert abs(sum(r[5] for r in res) - lb0) <= 1e-3 * abs(lb0)
+    # scalar gradients: the shards' contributions add up to the whole batch's within 1e-3, widened by twice the
+    # reordered-batch spread (a BT branch flip moves them as it moves y_bar above; the sharded and the
+    # single-process sums are two orderings, each within that spread of the others)
+    assert abs(sum(r[5] for r in res) - lb0) <= 1e-3 * abs(lb0) + 2 * spread["lam"], (sum(r[5] for r in res), lb0, spread)
     if need_rho:
-        assert _rel(sum(r[4] for r in res), hb0.cpu().numpy()) < 1e-3
-        assert abs(sum(r[6] for r in res) - float(rb0)) <= 1e-3 * abs(float(rb0))
+        hb0n = hb0.cpu().numpy()
+        dh = float(np.linalg.norm(sum(r[4] for r in res) - hb0n))
+        assert dh <= 1e-3 * float(np.linalg.norm(hb0n)) + 2 * spread["h"], (dh, spread)
+        assert abs(sum(r[6] for r in res) - float(rb0)) <= 1e-3 * abs(float(rb0)) + 2 * spread["rho"], spread
     else:
         assert rb0 is None and all(r[6] is None for r in res)

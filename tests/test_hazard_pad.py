@@ -67,3 +67,18 @@ def test_swap_writes_both_operands():
 def test_other_wide_store_forms(mn):
     _, n = pad("\t" + mn, "\tv_mov_b32_e32 v47, 0")
     assert n == 1
+
+
+def test_scratch_sizes_reads_kernel_descriptors():
+    """The build invariant check (__graft_entry__.TU_CHECKS) reads each kernel's scratch bytes from the
+    .amdhsa_kernel descriptors of the device assembly."""
+    import hazard_pad
+    asm = """\t.amdhsa_kernel _Z3fooPf
+\t\t.amdhsa_group_segment_fixed_size 0
+\t\t.amdhsa_private_segment_fixed_size 0
+\t.end_amdhsa_kernel
+\t.amdhsa_kernel _Z3barPf
+\t\t.amdhsa_private_segment_fixed_size 288
+\t.end_amdhsa_kernel
+"""
+    assert hazard_pad.scratch_sizes(asm) == {"_Z3fooPf": 0, "_Z3barPf": 288}
