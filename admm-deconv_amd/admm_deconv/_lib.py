@@ -9,7 +9,8 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # .../admm-deconv_amd
-LIB_PATH = os.path.join(PKG_ROOT, "libadmm_deconv.so")
+# ADMM_LIB_PATH: another build of the library for A/B timing experiments (tools/); default the in-tree build
+LIB_PATH = os.environ.get("ADMM_LIB_PATH") or os.path.join(PKG_ROOT, "libadmm_deconv.so")
 
 ADMM_OK = 0
 ADMM_E_INVALID = -1

@@ -221,8 +221,11 @@ class Parallel:
     workgroups, ISO_MERGE_MAX_PLANES, or with merge="always"), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
     planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
     each branch's bias and σ then apply to its slice.  The forward output, λ̄ and ρ̄ are bitwise those of the
-    branches run one by one; the input gradient matches them to fp32 rounding (branch_sum_kernel adds the
-    branches' ȳ in a fixed order, not in autograd's per-branch accumulation order).  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
+    branches run one by one through the same per-plane kernels (tests/test_gpu_multi.py, ADMM_OPT_MIN_PLANES = 0);
+    under the library's default plane-count rule a small branch alone runs the 2-pass kernels while the merged
+    grid runs the fused ones, so the two then agree to fp32 rounding, not bitwise (tests/test_gpu_default_rule.py).
+    The input gradient matches to fp32 rounding in either case (branch_sum_kernel adds the branches' ȳ in a
+    fixed order, not in autograd's per-branch accumulation order).  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
     (forward, and -- autograd replays a backward op on its forward's stream -- the adjoint too), then the
     caller's stream waits for all of them.  merge=False keeps the per-branch path; streams=False runs the
     branches one after the other on the caller's stream (the reference's single task-local stream)."""

@@ -100,6 +100,9 @@ def parse():
                     help="c5 --iso: the branches in one grid (ADMM_MULTI_ISO) at any batch (default: only when all their planes fit one wave of workgroups, layers.ISO_MERGE_MAX_PLANES)")
     ap.add_argument("--iso", action="store_true",
                     help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
+    ap.add_argument("--graph", action="store_true",
+                    help="c5: capture the whole training step (forward, loss, adjoint, update) in one HIP graph and "
+                         "replay it (small batches are launch-bound: the reference's train_cfg.json batch 2)")
     return ap.parse_args()
 
 
@@ -164,12 +167,29 @@ def bench_c5(args, dev):
                 L.lam.grad = None
         return loss
 
+    run = step
+    graph = None
+    if args.graph:
+        # warm up on a side stream (allocations, recordings registry, kernel attributes), then capture one whole
+        # step; replays re-run every kernel of it (the gradients are recomputed, not accumulated: grad is None
+        # going into the capture, so backward() writes fresh tensors from the graph's pool)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
     for _ in range(args.warmup):
-        step()
+        run()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     # per-kernel timing from a separate instrumented step with the branches serialised, so that each
@@ -271,7 +291,9 @@ def bench_c5(args, dev):
         "config": {"workload": f"c5: batch {B} of {M}x{N}x{P}, 5 x ADMMDeconvF2((), {K}, rho, relu1) + chcat, "
                                "GMSD loss (HIP), backward through the recorded adjoint "
                                f"({'iso' if args.iso else 'aniso'}; "
-                               f"{'branches in one grid' if merged else 'per-branch solves'})", "global_batch": B},
+                               f"{'branches in one grid' if merged else 'per-branch solves'}"
+                               f"{'; whole step replayed as one HIP graph' if graph is not None else ''})",
+                   "global_batch": B},
         "roofline": roof, "kernels": kernels}))
 
 

@@ -1,0 +1,111 @@
+"""GPU parity of the paths the library takes under its DEFAULT plane-count rule (ADMM_OPT_MIN_PLANES = -1,
+admm_paths.hip enough_planes): below a measured plane count the one-workgroup-per-plane kernels give way to
+the multi-workgroup 2-pass ones.  The rest of the GPU suite pins the per-plane kernels at every
+batch (conftest); here every threshold is crossed at the default rule, both sides checked against the fp64
+oracle.  Reference: /root/reference/src/ops/ops.jl:17-96 (forward),
+src/train.jl:51 (the recorded adjoint of training)."""
+import numpy as np
+import pytest
+import torch
+
+import admm_deconv
+from admm_deconv import _lib, layers, synth
+from parity import assert_parity_fp32ref, oracle_solve
+
+pytestmark = [pytest.mark.gpu, pytest.mark.min_planes_rule]
+
+# (id, side, iso, (psf size, sigma) or None, planes below, planes at, path below, path at, K, oracle planes)
+FWD = [
+    ("fused256", 256, False, (15, 2.5), 95, 96, "2pass", "fused", 25, 3),
+    ("fusediso256", 256, True, (15, 2.5), 111, 112, "2pass_iso", "fused_iso", 4, None),
+    ("resident250", 250, False, (15, 2.5), 128, 192, "smooth", "resident", 25, 2),
+    ("residentiso120", 120, True, (9, 1.5), 255, 256, "smooth", "resident_iso", 6, None),
+]
+
+
+def _solve(dev, y, h, iso, K):
+    x = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), 0.0041, 0.021, torch.from_numpy(h).to(dev), iso, K)
+    torch.cuda.synchronize()
+    return x.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", FWD, ids=[c[0] for c in FWD])
+def test_forward_both_sides_of_the_plane_rule(dev, case):
+    cid, side, iso, spec, nb, na, pb, pa, K, nor = case
+    assert _lib.get_option("MIN_PLANES") == -1
+    kh = spec[0]
+    assert _lib.query_paths(side, side, iso, kh, planes=nb)[0] == pb
+    assert _lib.query_paths(side, side, iso, kh, planes=na)[0] == pa
+    h = synth.gaussian_psf(*spec)
+    y = synth.make_batch(na, side, side, h, g0=21)
+    for n, path in ((nb, pb), (na, pa)):
+        got = _solve(dev, y[:n], h, iso, K)
+        what = f"{cid} {n} planes ({path})"
+        if iso:   # the prox couples the batch: the oracle solves all n planes
+            ref = oracle_solve(y[:n], 0.0041, 0.021, h, True, K, "spectral", what=what)
+            assert_parity_fp32ref(got, ref, y[:n], 0.0041, 0.021, h, True, K, what=what)
+        else:     # independent planes: the first few against the oracle
+            ref = oracle_solve(y[:nor], 0.0041, 0.021, h, False, K, "spectral", what=what)
+            assert_parity_fp32ref(got[:nor], ref, y[:nor], 0.0041, 0.021, h, False, K, what=what)
+        if n == nb:
+            below = got
+    if not iso:
+        # the planes both batches hold: two fp32 paths, each within 1e-5 of the oracle
+        a, b = below.reshape(nb, -1).astype(np.float64), got[:nb].reshape(nb, -1).astype(np.float64)
+        rel = np.linalg.norm(a - b, axis=1) / np.linalg.norm(b, axis=1)
+        assert rel.max() < 2e-5, f"{cid}: planes shared by the two batches differ by rel-L2 {rel.max():.2e}"
+
+
+def test_recorded_gradients_both_sides_of_the_plane_rule(dev):
+    """The training recording (mask bits, no rho_bar: the c5 layers) at 64 planes runs the 2-pass forward and
+    sweep, at 96 the fused ones (paths_table c5-record-masks-64 / -96).  The 64 planes of both agree: y_bar
+    trimmed per-plane rel-L2 <= 1e-4 and lambda_bar <= 5e-3 (tests/test_gpu_backward.py: fp32 mask flips near
+    the ST kink are the only difference), x <= 2e-5."""
+    from test_gpu_backward import assert_grad
+    M = 256
+    assert _lib.query_paths(M, M, False, 0, mode=_lib.MODE_RECORD, flags=_lib.REC_MASKS, planes=64) == \
+        ("2pass", "sweep_2pass")
+    assert _lib.query_paths(M, M, False, 0, mode=_lib.MODE_RECORD, flags=_lib.REC_MASKS, planes=96) == \
+        ("fused", "sweep_fused")
+    y = synth.make_batch(96, M, M, None, sigma=0.1, g0=5)
+    xbar = np.random.default_rng(3).standard_normal(y.shape).astype(np.float32)
+    out = {}
+    for n in (64, 96):
+        yt = torch.from_numpy(y[:n]).to(dev)
+        lam = torch.tensor([0.0041], device=dev)
+        x, rec = admm_deconv.tvd_fft_record(yt, lam, 0.021, None, False, 12, need_rho=False)
+        yb, _, lb, _ = admm_deconv.tvd_fft_backward_recorded(rec, x, torch.from_numpy(xbar[:n]).to(dev),
+                                                             need_rho=False)
+        torch.cuda.synchronize()
+        out[n] = (x.cpu().numpy(), yb.cpu().numpy(), float(lb))
+    xa, xb = out[64][0].astype(np.float64), out[96][0][:64].astype(np.float64)
+    assert np.linalg.norm(xa - xb) / np.linalg.norm(xb) < 2e-5
+    assert_grad(out[64][1], out[96][1][:64], "y_bar 64 (2-pass) vs 96 (fused)")
+    # lambda_bar sums over the planes: the 64-plane 2-pass sweep against the same 64 planes through the fused
+    # sweep (the per-plane kernels forced, MIN_PLANES = 0)
+    with _lib.option("MIN_PLANES", 0):
+        yt = torch.from_numpy(y[:64]).to(dev)
+        x, rec = admm_deconv.tvd_fft_record(yt, torch.tensor([0.0041], device=dev), 0.021, None, False, 12,
+                                            need_rho=False)
+        _, _, lbf, _ = admm_deconv.tvd_fft_backward_recorded(rec, x, torch.from_numpy(xbar[:64]).to(dev),
+                                                             need_rho=False)
+    assert abs(out[64][2] - float(lbf)) <= 5e-3 * abs(float(lbf)), (out[64][2], float(lbf))
+
+
+def test_merged_branches_vs_per_branch_at_the_default_rule(dev):
+    """Parallel's merged isotropic grid (fused kernels over all 5 branches' planes) against
+    the branches one by one, each small enough (3 planes) for the 2-pass isotropic kernels at the default rule:
+    the same solves through different paths agree to fp32 rounding (rel-L2 <= 2e-5 per plane), not bitwise."""
+    rng = np.random.default_rng(0)
+    branch = [layers.ADMMDeconvF2((), 8, r, layers.relu1, iso=True, rng=rng, device=dev) for r in (0.02, 0.2, 2.0)]
+    x = torch.from_numpy(synth.make_batch(1, 256, 256, None, P=3, sigma=0.1)).to(dev)
+    merged = layers.Parallel(layers.chcat, *branch)
+    assert merged._mergeable(x)
+    assert _lib.query_paths(256, 256, True, 0, planes=3)[0] == "2pass_iso"
+    with torch.no_grad():
+        a = merged(x).cpu().numpy().astype(np.float64)
+        b = layers.Parallel(layers.chcat, *branch, merge=False)(x).cpu().numpy().astype(np.float64)
+    a, b = a.reshape(-1, 256 * 256), b.reshape(-1, 256 * 256)
+    nz = np.linalg.norm(b, axis=1) > 0
+    rel = np.linalg.norm(a - b, axis=1)[nz] / np.linalg.norm(b, axis=1)[nz]
+    assert rel.max() <= 2e-5, rel
