@@ -275,12 +275,12 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 //   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar), in fp64:
 //            K terms per bin, later scaled by C^2 in hbarA_kernel
 // ----------------------------------------------------------------------------------------------
+// The body takes the block's (slot block, plane) explicitly so that a persistent kernel can run it too
+// (team512_kernel below); column_kernel is the one-launch-per-pass form.
 template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
-__global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst,
-                                                          const float* __restrict__ Ct,
-                                                          const float2* __restrict__ Gt,
-                                                          const float2* __restrict__ twN, int L, int KB, float cs,
-                                                          float2* __restrict__ vsave, double* __restrict__ Qp) {
+__device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* dst, const float* __restrict__ Ct,
+                                            const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
+                                            int KB, float cs, float2* __restrict__ vsave, double* __restrict__ Qp) {
     constexpr bool CPLX = MUL != 0;
     constexpr int FS = NN + 1;  // per-transform LDS stride (odd: conflict-free slot-major stores)
     constexpr int P = Plan<NN>::P;
@@ -288,7 +288,6 @@ __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* d
     float2* tw = reinterpret_cast<float2*>(smem_raw);
     float2* S0 = tw + NN;        // slot-0 spectrum for the mirror term
     float2* buf = S0 + NN;
-    const XBlk xb = xcd_block();
     const int plane = xb.y;
     const int k0 = xb.x * KB;
     const int H = L + 1;
@@ -466,31 +465,37 @@ __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* d
     }
 }
 
+template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
+__global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst, const float* __restrict__ Ct,
+                                                    const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
+                                                    int KB, float cs, float2* __restrict__ vsave,
+                                                    double* __restrict__ Qp) {
+    column_body<NN, MUL, SAVE, ACCQ, NT>(xcd_block(), src, dst, Ct, Gt, twN, L, KB, cs, vsave, Qp);
+}
+
 // ----------------------------------------------------------------------------------------------
 // LINE pass (iterations 1..K-1): T output lines + 1 halo line on each side.
 // ----------------------------------------------------------------------------------------------
-template <int L, int T>
-__global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict__ spec1, float2* __restrict__ spec0,
-                                                        const float* __restrict__ s_old, float* __restrict__ s_new,
-                                                        const float* __restrict__ hty,
-                                                        const float2* __restrict__ twM, int N, const float* __restrict__ prm,
-                                                        int s_zero) {
+template <int L, int T, int NT = kThreads>
+__device__ __forceinline__ void line_body(XBlk xb, const float2* __restrict__ spec1, float2* __restrict__ spec0,
+                                          const float* __restrict__ s_old, float* __restrict__ s_new,
+                                          const float* __restrict__ hty, const float2* __restrict__ twM, int N,
+                                          const float* __restrict__ prm, int s_zero) {
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
     constexpr int P = Plan<L>::P;
     constexpr int NE = (T + 1) * M4;                       // float4 items of the elementwise step
-    constexpr int NIT = (NE + kThreads - 1) / kThreads;
+    constexpr int NIT = (NE + NT - 1) / NT;
     constexpr int RF = plan_radix<L, 0, true>();           // forward (reversed plan) first radix
     constexpr int QF = L / RF;
-    constexpr int NITF = (T * QF + kThreads - 1) / kThreads;
+    constexpr int NITF = (T * QF + NT - 1) / NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
     float2* X = tw + M;           // TH lines
     float2* Bf = X + TH * L;      // TH lines
     float2* Cf = Bf + TH * L;     // TH lines (w1; 3rd ping-pong buffer for 3-pass plans)
-    const XBlk xb = xcd_block();
     const int plane = xb.y;
     const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
@@ -504,13 +509,13 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     // VGPRs) so that 4-line blocks run 4 per CU (c4 line pass 1.173 -> 1.140 ms); at 256
     // points the early loads win (0.192 vs 0.201 ms) ----
     constexpr bool kJit = L == 256;
-    for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
+    for (int t = tid; t < M; t += NT) tw[t] = twM[t];
     load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
     float4 pre0[NIT], pre1[NIT];
     auto load_s = [&] {
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
-            const int idx = tid + it * kThreads;
+            const int idx = tid + it * NT;
             const int t = idx / M4;
             const int i = (idx - t * M4) * 4;
             const size_t off = (size_t)((j0 + t) & (N - 1)) * M + i;
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     auto load_h = [&] {
 #pragma unroll
         for (int it = 0; it < NITF; ++it) {
-            const int idx = tid + it * kThreads;
+            const int idx = tid + it * NT;
             const int f = idx / QF, j = idx - f * QF;
             if (idx < T * QF) {
                 const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
@@ -570,7 +575,7 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     // ---- s = Dx + u_old ; w = z - u   (ops.jl:169-173) ----
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-        const int idx = tid + it * kThreads;
+        const int idx = tid + it * NT;
         if (idx < NE) {
             const int t = idx / M4;
             const int i = (idx - t * M4) * 4;
@@ -606,7 +611,7 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
     float2* F0 = const_cast<float2*>(Xr);   // x is dead now
 #pragma unroll
     for (int it = 0; it < NITF; ++it) {
-        const int idx = tid + it * kThreads;
+        const int idx = tid + it * NT;
         if (idx < T * QF) {
             const int f = idx / QF, j = idx - f * QF;
             const float* w0a = W0 + f * M;
@@ -652,6 +657,101 @@ __global__ __launch_bounds__(kThreads) void line_kernel(const float2* __restrict
         Z = Cf;
     }
     pack_store<L>(Z, spec0 + (size_t)plane * N * L, j0, T, N, tw);
+}
+
+template <int L, int T, int NT = kThreads>
+__global__ __launch_bounds__(NT) void line_kernel(const float2* __restrict__ spec1, float2* __restrict__ spec0,
+                                                  const float* __restrict__ s_old, float* __restrict__ s_new,
+                                                  const float* __restrict__ hty, const float2* __restrict__ twM, int N,
+                                                  const float* __restrict__ prm, int s_zero) {
+    line_body<L, T, NT>(xcd_block(), spec1, spec0, s_old, s_new, hty, twM, N, prm, s_zero);
+}
+
+// ----------------------------------------------------------------------------------------------
+// TEAM512 (experiment, round 5; VERDICT r04 Next #4): the 2-pass solve at 512 x 512 as ONE persistent
+// launch.  Four 1024-thread workgroups (a "team", placed on one XCD by the dispatch order: workgroup b runs
+// on XCD b mod 8) solve one plane at a time, all K iterations: each member runs the column pass on a quarter
+// of the plane's spectral slots and the line pass on a quarter of its lines, with a team barrier in place of
+// every kernel boundary.  The spectrum still moves through global memory between the passes -- the
+// question this prototype answers is whether it then stays in the XCD's L2 / the Infinity Cache (one plane's
+// 1 MiB per team at a time, 64 planes in flight) instead of streaming from HBM (16 of the 2-pass form's
+// 36 B/px per iteration).  Same bodies as column_kernel / line_kernel, so the same results bit for bit.
+// Team barrier (cdna_hip_programming.md Guideline 16, counter form): every wave drains its stores, one lane
+// releases at agent scope, adds to the team's counter and polls it relaxed; one agent acquire after the
+// match.  Every spin is bounded: on a timeout the lane sets err[0] and every later wait of every team
+// returns at once, so the grid always drains (results are then invalid; the host reports the flag).
+__device__ __forceinline__ void team_barrier(unsigned* cnt, unsigned target, unsigned* err) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) {   // ~0.5 s: a member is not resident
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+constexpr int kTeamSize = 4, kTeamThreads = 1024, kTeamKB = 16, kTeamT = 16;
+__device__ unsigned g_team512_sync[1024];   // team counters + error word (experiment: one call at a time)
+
+// The two phases as real calls: inlined into the persistent loop, the compiler hoists loop-invariant work of both
+// bodies and the kernel spilled 196 B/lane at the 128-VGPR cap of 1024-thread workgroups (each phase alone: 0)
+__device__ __attribute__((noinline)) void team_column(XBlk xb, const float2* src, float2* dst, const float* Ct,
+                                                      const float2* twN, float cs) {
+    column_body<512, 0, false, false, kTeamThreads>(xb, src, dst, Ct, nullptr, twN, 256, kTeamKB, cs, nullptr, nullptr);
+}
+__device__ __attribute__((noinline)) void team_line(XBlk xb, const float2* spec1, float2* spec0, const float* so, float* sn,
+                                                    const float* hty, const float2* twM, const float* prm, int s_zero) {
+    line_body<256, kTeamT, kTeamThreads>(xb, spec1, spec0, so, sn, hty, twM, 512, prm, s_zero);
+}
+
+// grid = a multiple of 32 workgroups, all resident (cooperative launch); sync = nteams counters + err word, zeroed
+__global__ __launch_bounds__(kTeamThreads) void team512_kernel(const float2* first, float2* spec0, float2* spec1,
+                                                               float* sA, float* sB, const float* __restrict__ hty,
+                                                               const float* __restrict__ Ct, const float2* __restrict__ twM,
+                                                               const float2* __restrict__ twN, const float* __restrict__ prm,
+                                                               int planes, int K, float cs1, unsigned* sync) {
+    constexpr int NN = 512, L = 256;
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int x = b & 7, l = b >> 3;                 // XCD, slot on it
+    const int tpx = nwg / 8 / kTeamSize;             // teams per XCD
+    const int team = x * tpx + l / kTeamSize, member = l % kTeamSize;
+    const int nteams = nwg / kTeamSize;
+    unsigned* cnt = sync + team;
+    unsigned* err = sync + nteams;
+    unsigned target = 0;
+    constexpr int kColBlocks = L / kTeamKB / kTeamSize;   // 4 slot blocks of 16 per member
+    constexpr int kLineBlocks = NN / kTeamT / kTeamSize;  // 8 line blocks of 16 per member
+    for (int p = team; p < planes; p += nteams) {
+        for (int it = 1; it <= K; ++it) {
+            for (int c = 0; c < kColBlocks; ++c) {
+                team_column(XBlk{member * kColBlocks + c, p}, it == 1 ? first : spec0, spec1, Ct, twN, it == 1 ? cs1 : 1.0f);
+                __syncthreads();
+            }
+            target += kTeamSize;
+            team_barrier(cnt, target, err);
+            if (it == K) break;
+            float* so = (it & 1) ? sB : sA;   // iteration 1 reads nothing (s_zero)
+            float* sn = (it & 1) ? sA : sB;
+            for (int c = 0; c < kLineBlocks; ++c) {
+                team_line(XBlk{member * kLineBlocks + c, p}, spec1, spec0, so, sn, hty, twM, prm, it == 1 ? 1 : 0);
+                __syncthreads();
+            }
+            target += kTeamSize;
+            team_barrier(cnt, target, err);
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------------------------

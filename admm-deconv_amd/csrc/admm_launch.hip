@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "capi_internal.hpp"
@@ -65,7 +67,18 @@ int launch_line_inv(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
 
 int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float2* spec0,
                 const float* so, float* sn, const float* hty, const float2* twM, int N, const float* prm,
-                int sz) {
+                int sz, int nt = kThreads) {
+    if (nt != kThreads) {   // wider blocks at 512-point lines (update kernel, line_T_upd)
+#define X(l, t, n)                                                                                       \
+        if (L == l && T == t && nt == n) {                                                               \
+            set_lds(line_kernel<l, t, n>, lds);                                                          \
+            line_kernel<l, t, n><<<g, n, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz);         \
+            return 0;                                                                                    \
+        }
+        X(256, 8, 512) X(256, 16, 1024) X(256, 4, 512) X(256, 8, 1024)
+#undef X
+        return -1;
+    }
 #define X(l, t)                                                                                          \
     if (L == l && T == t) {                                                                              \
         set_lds(line_kernel<l, t>, lds);                                                                 \
@@ -75,6 +88,34 @@ int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* s
     ADMM_LT_CASES(X)
 #undef X
     return -1;
+}
+
+// the persistent 512 x 512 team launch (admm_kernels.hip team512_kernel; experiment): every workgroup resident
+// (cooperative launch), whole teams of 4 per XCD, counters zeroed per call
+int launch_team512(hipStream_t s, const float2* first, float2* spec0, float2* spec1, float* sA, float* sB,
+                   const float* hty, const float* Ct, const float2* twM, const float2* twN, const float* prm, int planes,
+                   int K, float cs1) {
+    const size_t lds = std::max(line_lds(512, kTeamT), (size_t)512 * 16 + (size_t)kTeamKB * 513 * 8);
+    static int nwg = -1;
+    if (nwg < 0) {
+        set_lds(team512_kernel, lds);
+        int per = 0, dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, team512_kernel, kTeamThreads, lds) != hipSuccess) per = 0;
+        nwg = per * cus / (8 * kTeamSize) * (8 * kTeamSize);
+    }
+    if (nwg < 8 * kTeamSize) return fail(ADMM_E_UNSUPPORTED, "team512: no resident grid (%d workgroups)", nwg);
+    void* sync = nullptr;
+    hipError_t e = hipGetSymbolAddress(&sync, HIP_SYMBOL(g_team512_sync));
+    if (e == hipSuccess) e = hipMemsetAsync(sync, 0, (size_t)(nwg / kTeamSize + 1) * 4, s);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "team512 sync: %s", hipGetErrorString(e));
+    unsigned* sy = static_cast<unsigned*>(sync);
+    void* args[] = {&first, &spec0, &spec1, &sA, &sB, &hty, &Ct, &twM, &twN, &prm, &planes, &K, &cs1, &sy};
+    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(team512_kernel), dim3(nwg), dim3(kTeamThreads), args,
+                                   (unsigned)lds, s);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "team512 cooperative launch (%d workgroups): %s", nwg, hipGetErrorString(e));
+    return 0;
 }
 
 int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* so, float* sn,
@@ -302,7 +343,14 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     const int KB = column_KB(M, N);
     // the per-iteration line update runs 4-line blocks at 512-point lines (its just-in-time loads let 4 of
     // them share a CU, admm_kernels.hip line_kernel); the one-off line transforms keep T
-    const int Tu = (M == 512 && T > 4) ? 4 : T;
+    int Tu = (M == 512 && T > 4) ? 4 : T;
+    int nTu = kThreads;
+    // experiment (r05): wider update blocks at 512-point lines, ADMM_EXP_LINE512 = "T,threads"
+    if (M == 512) {
+        static const char* e = getenv("ADMM_EXP_LINE512");
+        int et = 0, en = 0;
+        if (e && sscanf(e, "%d,%d", &et, &en) == 2 && et > 0 && en > 0) { Tu = et; nTu = en; }
+    }
     const size_t llds = line_lds(M, Tu), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
     float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
@@ -328,6 +376,9 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                                     maxit, opt(ADMM_OPT_PLANE_STAGGER));
         });
     }
+    // experiment (round 5): the 512 x 512 anisotropic solve as one persistent team launch (team512_kernel)
+    static const bool team512 = getenv("ADMM_EXP_TEAM512") && atoi(getenv("ADMM_EXP_TEAM512")) > 0;
+    const bool use_team = team512 && M == 512 && N == 512 && !iso && !tr.s && !tr.v;
     // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
     rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
     if (rc) return rc;
@@ -342,6 +393,13 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         cs1 = (float)M;
     }
     const size_t sstride = np * 2 * MN;   // one trajectory slot of s
+    if (use_team) {
+        rc = ln.run(ADMM_K_PLANE, [&] {
+            return launch_team512(s, first, spec0, spec1, sbuf[0], sbuf[1], hty, Ct, twM, twN, prm, (int)np, maxit, cs1);
+        });
+        if (rc) return rc;
+        return ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
+    }
     for (int it = 1; it <= maxit; ++it) {
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * np * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
@@ -361,7 +419,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
             }
             rc = ln.run(ADMM_K_LINE, [&] {
                 return launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, hty, twM, N, prm,
-                            it == 1 ? 1 : 0);
+                            it == 1 ? 1 : 0, nTu);
             });
         } else if (it < maxit) {
             // isotropic: s is written in place (no halo reads of s in ISO_A); with a trajectory each

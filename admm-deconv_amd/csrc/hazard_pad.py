@@ -144,6 +144,13 @@ def compile_tu(src, obj, flags, verbose=False, scratch_out=None):
     steps = [l for l in r.stderr.split("\n") if l.startswith(' "')]
     if r.returncode != 0 or not steps:
         raise RuntimeError(f"hipcc -### failed for {src}:\n{r.stderr[-2000:]}")
+    try:
+        return _run_steps(steps, work, src, verbose, scratch_out)
+    finally:
+        shutil.rmtree(work, ignore_errors=True)   # also after a failed step (no .hipi left in the tree)
+
+
+def _run_steps(steps, work, src, verbose, scratch_out):
     total = 0
     for i, step in enumerate(steps):
         is_dev_as = "-cc1as" in step and "amdgcn-amd-amdhsa" in step
@@ -164,5 +171,4 @@ def compile_tu(src, obj, flags, verbose=False, scratch_out=None):
             raise RuntimeError(f"build step {i} failed for {src}:\n{err[-3000:]}")
         if verbose and err:
             print(err)
-    shutil.rmtree(work, ignore_errors=True)
     return total
