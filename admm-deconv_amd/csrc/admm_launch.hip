@@ -343,9 +343,11 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     const int KB = column_KB(M, N);
     // the per-iteration line update runs 4-line blocks at 512-point lines (its just-in-time loads let 4 of
     // them share a CU, admm_kernels.hip line_kernel); the one-off line transforms keep T
-    int Tu = (M == 512 && T > 4) ? 4 : T;
-    int nTu = kThreads;
-    // experiment (r05): wider update blocks at 512-point lines, ADMM_EXP_LINE512 = "T,threads"
+    // 512-point lines: 8-line update blocks of 512 threads (round 5, tools/c4_line_sweep.sh: line pass 1.217 ->
+    // 1.196 ms at c4; 4 lines x 256 threads was round 1's choice; 16 x 1024, 4 x 512 and 8 x 1024 slower:
+    // profiles/r05_c4_line_sweep.jsonl).  ADMM_EXP_LINE512 = "T,threads" overrides (experiments)
+    int Tu = (M == 512 && T > 4) ? 8 : T;
+    int nTu = (M == 512 && Tu == 8) ? 512 : kThreads;
     if (M == 512) {
         static const char* e = getenv("ADMM_EXP_LINE512");
         int et = 0, en = 0;
