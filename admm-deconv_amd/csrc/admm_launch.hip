@@ -157,6 +157,14 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
     ADMM_N_CASES(X)
 #undef X
 #define X(v)                                                                                                   \
+    if (N == v && nt == 512) {                                                                                 \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 512>, lds);                                                  \
+        column_kernel<v, MUL, SAVE, ACCQ, 512><<<g, 512, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp);  \
+        return 0;                                                                                              \
+    }
+    X(256) X(512) X(1024)
+#undef X
+#define X(v)                                                                                                   \
     if (N == v && nt == 1024) {                                                                                \
         set_lds(column_kernel<v, MUL, SAVE, ACCQ, 1024>, lds);                                                 \
         column_kernel<v, MUL, SAVE, ACCQ, 1024><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \

@@ -51,7 +51,7 @@ int max_q(int NN) {
 int column_threads(int N) {
     int nt = N >= 512 ? 1024 : 256;
     const int v = opt(ADMM_OPT_COL_THREADS);
-    if (v == 256 || (v == 1024 && N >= 256)) nt = v;
+    if (v == 256 || ((v == 512 || v == 1024) && N >= 256)) nt = v;
     return nt;
 }
 int column_KB(int M, int N) {

@@ -44,6 +44,16 @@ from admm_deconv import _lib, parallel, synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def achievable_gbs():
+    """The best rate a hand-written gfx950 stream of the solve kernels' own 12:8 read/write mix reaches
+    (tools/ubench/stream.hip, profiles/r05_hbm_ceiling.json), or None."""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "r05_hbm_ceiling.json")))
+        return 1000.0 * float(d["achievable_mixed_TBps"])
+    except Exception:   # noqa: BLE001
+        return None
+
+
 def canonical_bytes(M, N, K):
     """per plane K*[32*(M/2+1)*N + 20*M*N] + 12*M*N."""
     return K * (32 * (M // 2 + 1) * N + 20 * M * N) + 12 * M * N
@@ -528,6 +538,9 @@ def main():
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # against the measured streaming ceiling of the same read/write mix (not the 8 TB/s spec)
+        "achievable_peak": achievable_gbs(),
+        "frac_of_achievable": round(ach / achievable_gbs(), 4) if achievable_gbs() else None,
         "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
         "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
         "compute": compute_side(config, dom, kernels[dom]["avg_ms"]),

@@ -234,7 +234,7 @@ enum {
     ADMM_OPT_FUSED = 0,          /* 1 (default): fused per-plane kernel at 256x256 anisotropic; 0: 2-pass */
     ADMM_OPT_FUSED_ADJ = 1,      /* 1 (default): fused reverse sweep on a fused trajectory; 0: 2-pass    */
     ADMM_OPT_LINE_T = 2,         /* 0 (default): tile policy; 2/4/8/16: cap on lines per line block      */
-    ADMM_OPT_COL_THREADS = 3,    /* 0 (default): policy; 256 or 1024 threads per column block            */
+    ADMM_OPT_COL_THREADS = 3,    /* 0 (default): policy; 256, 512 or 1024 threads per column block       */
     ADMM_OPT_GEN_TM = 4,         /* 0 (default 2048): runtime-length line block points, 256..8192        */
     ADMM_OPT_GEN_KN = 5,         /* 0 (default 1024): runtime-length column block points, 256..8192      */
     ADMM_OPT_PLANE_STAGGER = 6,  /* 0 (default): fused kernel odd-workgroup start delay, 10 ns ticks     */
