@@ -404,8 +404,10 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
                                                              float* __restrict__ vsum, float* __restrict__ rpartial,
                                                              double* __restrict__ part, const float2* __restrict__ twM,
                                                              int N, int planes, int G, const float* __restrict__ prm,
-                                                             int first_k, int last_k) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
+                                                             int first_k, int last_k, Branches br = kOneSolve,
+                                                             int ngb = 0, size_t pbs = 0) {
+    // several branches (admm_kernels.hip Branches): planes per branch, ngb plane groups per branch (grid y =
+    // branches x ngb), pbs doubles between the branches' partial-row blocks; xK in the chcat layout
     // nrm1 = Nrm_{k-1} (k >= 2), nrm0 = Nrm_{k-2} (k >= 3; for D x_k = s_k - psi(s_{k-1}) we need f_{k-1}
     // only: nrm0 is unused but kept for symmetry of the call -- psi(s_{k-1}) uses nrm1)
     (void)nrm0;
@@ -423,7 +425,13 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
     const XBlk xb = xcd_block();
     const int j0 = xb.x * T;
     const int grp = xb.y;
+    const int nb_ = ngb > 0 ? ngb : (int)gridDim.y;
+    const int bri = grp / nb_, gl = grp - bri * nb_;
     const size_t MN = (size_t)M * N;
+    if (nrm1) nrm1 += (size_t)bri * MN;
+    prm += (size_t)bri * br.prm_f;
+    part += (size_t)bri * pbs;
+    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
     const int tid = threadIdx.x;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     float4 racc[NIT], fo[NIT];
@@ -439,8 +447,8 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
         }
     }
     float rho_acc = 0.0f;
-    const int p_end = min(planes, (grp + 1) * G);
-    for (int plane = grp * G; plane < p_end; ++plane) {
+    const int p_end = bri * planes + min(planes, (gl + 1) * G);
+    for (int plane = bri * planes + gl * G; plane < p_end; ++plane) {
         __syncthreads();
         load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
         __syncthreads();
@@ -486,7 +494,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
             // (xK / sk null: rho_bar not wanted, D x_k reads as 0 and costs no traffic)
             float dx0[4] = {0, 0, 0, 0}, dx1[4] = {0, 0, 0, 0};
             if (last_k && xK) {
-                const float* xp = xK + (size_t)plane * MN;
+                const float* xp = xK + branch_of(br, plane).out_plane * MN;
                 const float4 xc = *reinterpret_cast<const float4*>(xp + off);
                 const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
                 const float xl = xp[(size_t)(j0 + t) * M + ((i - 1) & (M - 1))];
@@ -547,14 +555,21 @@ __global__ __launch_bounds__(kThreads) void iso_adj_a_kernel(const float2* __res
         }
     }
     __syncthreads();
-    block_sum2(rho_acc, 0.0f, part + 2 * ((size_t)grp * gridDim.x + xb.x), red);
+    block_sum2(rho_acc, 0.0f, part + 2 * ((size_t)gl * gridDim.x + xb.x), red);
 }
 
 // R map = sum over plane groups of the partial sums; tau_bar partials (block-reduced, one pair per block)
+// grid (blocks, branches): branch blockIdx.y sums its own ngroups partials; its tau_bar rows pbs doubles on
 __global__ __launch_bounds__(kThreads) void iso_adj_r_kernel(const float* __restrict__ rpartial, float* __restrict__ Rmap,
                                                              const float* __restrict__ nrm1, int ngroups, size_t MN,
-                                                             const float* __restrict__ prm, double* __restrict__ part) {
-    const float tau = prm[0];   // device-resident scalars (setup_kernel)
+                                                             const float* __restrict__ prm, double* __restrict__ part,
+                                                             unsigned prm_f = 0, size_t pbs = 0) {
+    const size_t bi = blockIdx.y;
+    rpartial += bi * ngroups * MN;
+    Rmap += bi * MN;
+    nrm1 += bi * MN;
+    part += bi * pbs;
+    const float tau = prm[bi * prm_f];   // device-resident scalars (setup_kernel)
     __shared__ double red[2 * (kThreads / 64)];
     __shared__ float gred[kThreads];
     float tacc = 0.0f;
@@ -576,8 +591,7 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
                                                              const float* __restrict__ sk1, const float* __restrict__ nrm1,
                                                              const float* __restrict__ Rmap, float* __restrict__ sb_out,
                                                              float2* __restrict__ spec0, const float2* __restrict__ twM,
-                                                             int N, const float* __restrict__ prm) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
+                                                             int N, const float* __restrict__ prm, Branches br = kOneSolve) {
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;
@@ -596,6 +610,10 @@ __global__ __launch_bounds__(kThreads) void iso_adj_b_kernel(const float* __rest
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const size_t poff = (size_t)plane * 2 * MN;
+    const int bri = branch_of(br, plane).i;
+    nrm1 += (size_t)bri * MN;
+    Rmap += (size_t)bri * MN;
+    const float tau = prm[(size_t)bri * br.prm_f], rho = prm[(size_t)bri * br.prm_f + 1];   // (setup_kernel)
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     for (int idx = tid; idx < NE; idx += kThreads) {
         const int t = idx / M4, i = (idx - t * M4) * 4;

@@ -29,11 +29,27 @@
 #include <stdint.h>
 
 #include "fft_reg.hpp"
+#include "plane_api.hpp"
 #include "scalar_src.hpp"
 
 namespace admm {
 
 constexpr int kThreads = 256;
+// Several branches in one grid (admm_launch.hip launch_forward_multi below the plane-count rule): grid plane
+// q = i ppb + loc is branch i's solve of input plane loc; its output plane is the chcat position
+// (plane::branch_of).  The 2-pass kernels take per-branch C tables tab_f floats apart, {tau, rho, lambda}
+// blocks prm_f floats apart and per-branch M x N maps (f, |s|, R) M N floats apart.  nbr = 1: one solve.
+using plane::Branches;
+using plane::BranchOf;
+using plane::branch_of;
+constexpr Branches kOneSolve{1, 1, 1, 0u, 0u};
+// source / destination plane of a line transform: the grid plane, the shared input plane, or the chcat plane
+enum PlaneMap { kMapGrid = 0, kMapIn = 1, kMapOut = 2 };
+__device__ __forceinline__ size_t map_plane(const Branches& br, int map, size_t plane) {
+    if (map == kMapGrid || br.nbr == 1) return plane;
+    const BranchOf bo = branch_of(br, plane);
+    return map == kMapIn ? bo.in_plane : bo.out_plane;
+}
 constexpr int kSetupPsfLds = 4096;   // PSF taps the setup kernel stages in LDS (larger PSFs are read from global)
 
 // XCD-aware block order (2-D grid (x, y) -> logical (x, y)).  Workgroups are dealt round-robin over
@@ -219,7 +235,8 @@ __device__ __forceinline__ float prox_w(float s, float tau) {
 // ----------------------------------------------------------------------------------------------
 template <int L, int T>
 __global__ __launch_bounds__(kThreads) void line_fwd_kernel(const float* __restrict__ src, float2* __restrict__ spec,
-                                                            const float2* __restrict__ twM, int N) {
+                                                            const float2* __restrict__ twM, int N,
+                                                            Branches br = kOneSolve, int map = kMapGrid) {
     constexpr int M = 2 * L;
     constexpr int P = Plan<L>::P;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void line_fwd_kernel(const float* __restr
     const int j0 = xb.x * T;
     for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
     __syncthreads();
-    const float2* sp = reinterpret_cast<const float2*>(src + (size_t)plane * N * M);
+    const float2* sp = reinterpret_cast<const float2*>(src + map_plane(br, map, plane) * N * M);
     auto gload = [&](int f, int n) { return sp[(size_t)(j0 + f) * L + n]; };
     float2* Z = (P == 2) ? Bf : X;
     fft_plan<L, true, false, 2>(T, tw, X, Bf, L, gload, LdsIO{Z, L});
@@ -244,7 +261,8 @@ __global__ __launch_bounds__(kThreads) void line_fwd_kernel(const float* __restr
 // ----------------------------------------------------------------------------------------------
 template <int L, int T>
 __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __restrict__ spec, float* __restrict__ dst,
-                                                            const float2* __restrict__ twM, int N) {
+                                                            const float2* __restrict__ twM, int N,
+                                                            Branches br = kOneSolve, int map = kMapGrid) {
     constexpr int M = 2 * L;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* tw = reinterpret_cast<float2*>(smem_raw);
@@ -256,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
     for (int t = threadIdx.x; t < M; t += blockDim.x) tw[t] = twM[t];
     load_lines<L>(spec + (size_t)plane * N * L, X, j0, T, N);
     __syncthreads();
-    float2* dp = reinterpret_cast<float2*>(dst + (size_t)plane * N * M);
+    float2* dp = reinterpret_cast<float2*>(dst + map_plane(br, map, plane) * N * M);
     auto uload = [&](int f, int n) { return unpack_z<L>(X + f * L, n, tw); };
     auto gstore = [&](int f, int n, float2 v) { dp[(size_t)(j0 + f) * L + n] = v; };
     fft_plan<L, false, true, 2>(T, tw, Bf, X, L, uload, gstore);
@@ -469,8 +487,10 @@ template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
 __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst, const float* __restrict__ Ct,
                                                     const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
                                                     int KB, float cs, float2* __restrict__ vsave,
-                                                    double* __restrict__ Qp) {
-    column_body<NN, MUL, SAVE, ACCQ, NT>(xcd_block(), src, dst, Ct, Gt, twN, L, KB, cs, vsave, Qp);
+                                                    double* __restrict__ Qp, Branches br = kOneSolve) {
+    const XBlk xb = xcd_block();
+    column_body<NN, MUL, SAVE, ACCQ, NT>(xb, src, dst, Ct + (size_t)branch_of(br, xb.y).i * br.tab_f, Gt, twN, L, KB,
+                                         cs, vsave, Qp);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -771,7 +791,9 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
                                                          const float* s_old, float* s_new,
                                                          const float* __restrict__ fmap, float* __restrict__ part,
                                                          const float2* __restrict__ twM, int N, int planes, int G,
-                                                         int s_zero) {
+                                                         int s_zero, int ngb = 0) {
+    // planes: per branch; ngb: plane groups per branch (grid y = branches x ngb; 0: one branch).  Group g of branch
+    // i sums planes i planes + g G ..; its partial map stays at its grid row, f at the branch's map
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 1;           // one halo line on the left (x[j-1])
@@ -785,7 +807,10 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
     const XBlk xb = xcd_block();
     const int j0 = xb.x * T;
     const int grp = xb.y;
+    const int nb_ = ngb > 0 ? ngb : (int)gridDim.y;
+    const int bi = grp / nb_, gl = grp - bi * nb_;
     const size_t MN = (size_t)M * N;
+    fmap += (size_t)bi * MN;
     const int tid = threadIdx.x;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     float4 acc[NIT], fo[NIT];
@@ -797,8 +822,8 @@ __global__ __launch_bounds__(kThreads) void iso_a_kernel(const float2* __restric
         fo[it] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (!s_zero && idx < NE) fo[it] = *reinterpret_cast<const float4*>(fmap + (size_t)(j0 + t) * M + i);
     }
-    const int p_end = min(planes, (grp + 1) * G);
-    for (int plane = grp * G; plane < p_end; ++plane) {
+    const int p_end = bi * planes + min(planes, (gl + 1) * G);
+    for (int plane = bi * planes + gl * G; plane < p_end; ++plane) {
         __syncthreads();   // previous plane's LDS readers are done
         load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
         __syncthreads();
@@ -887,9 +912,15 @@ __device__ __forceinline__ float group_sum(const float* __restrict__ part, int n
     return r;
 }
 
+// grid (blocks, branches): branch blockIdx.y sums its own ngroups partials (iso_a's groups of that branch)
 __global__ __launch_bounds__(kThreads) void iso_r_kernel(const float* __restrict__ part, float* __restrict__ fmap,
-                                                         int ngroups, size_t MN, const float* __restrict__ prm, float* __restrict__ nrm_out) {
-    const float tau = prm[0];   // device-resident scalars (setup_kernel)
+                                                         int ngroups, size_t MN, const float* __restrict__ prm, float* __restrict__ nrm_out,
+                                                         unsigned prm_f = 0) {
+    const size_t bi = blockIdx.y;
+    part += bi * ngroups * MN;
+    fmap += bi * MN;
+    if (nrm_out) nrm_out += bi * MN;
+    const float tau = prm[bi * prm_f];   // device-resident scalars (setup_kernel)
     __shared__ float red[kThreads];
     for (size_t base = (size_t)blockIdx.x * 64; base < MN; base += (size_t)gridDim.x * 64) {
         const size_t q = base + (threadIdx.x & 63);
@@ -927,8 +958,8 @@ __global__ __launch_bounds__(kThreads) void iso_fin_kernel(float* __restrict__ f
 template <int L, int T>
 __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict__ s_new, const float* __restrict__ fmap,
                                                          const float* __restrict__ hty, float2* __restrict__ spec0,
-                                                         const float2* __restrict__ twM, int N, const float* __restrict__ prm) {
-    const float rho = prm[1];   // device-resident scalars (setup_kernel)
+                                                         const float2* __restrict__ twM, int N, const float* __restrict__ prm,
+                                                         Branches br = kOneSolve) {
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int P = Plan<L>::P;
@@ -946,8 +977,11 @@ __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict
     const int j0 = xb.x * T;
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
+    const BranchOf bo = branch_of(br, plane);
+    fmap += (size_t)bo.i * MN;
+    const float rho = prm[(size_t)bo.i * br.prm_f + 1];   // device-resident scalars (setup_kernel)
     const float* sp = s_new + (size_t)plane * 2 * MN;
-    const float* hp = hty + (size_t)plane * MN;
+    const float* hp = hty + bo.in_plane * MN;
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     for (int idx = tid; idx < NE; idx += kThreads) {
         const int t = idx / M4, i = (idx - t * M4) * 4;

@@ -39,13 +39,15 @@ void set_lds(K kernel, size_t lds) {
     X(512, 2) X(512, 4)
 #define ADMM_N_CASES(X) X(2) X(4) X(8) X(16) X(32) X(64) X(128) X(256) X(512) X(1024)
 
+// br / map (several branches in one grid): the line transforms read / write the shared input plane or the chcat
+// plane of each grid plane (admm_kernels.hip PlaneMap)
 int launch_line_fwd(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* src, float2* spec,
-                    const float2* twM, int N) {
-#define X(l, t)                                                            \
-    if (L == l && T == t) {                                                \
-        set_lds(line_fwd_kernel<l, t>, lds);                               \
-        line_fwd_kernel<l, t><<<g, kThreads, lds, s>>>(src, spec, twM, N); \
-        return 0;                                                          \
+                    const float2* twM, int N, const Branches& br = kOneSolve, int map = kMapGrid) {
+#define X(l, t)                                                                     \
+    if (L == l && T == t) {                                                         \
+        set_lds(line_fwd_kernel<l, t>, lds);                                        \
+        line_fwd_kernel<l, t><<<g, kThreads, lds, s>>>(src, spec, twM, N, br, map); \
+        return 0;                                                                   \
     }
     ADMM_LT_CASES(X)
 #undef X
@@ -53,12 +55,12 @@ int launch_line_fwd(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
 }
 
 int launch_line_inv(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec, float* dst,
-                    const float2* twM, int N) {
-#define X(l, t)                                                            \
-    if (L == l && T == t) {                                                \
-        set_lds(line_inv_kernel<l, t>, lds);                               \
-        line_inv_kernel<l, t><<<g, kThreads, lds, s>>>(spec, dst, twM, N); \
-        return 0;                                                          \
+                    const float2* twM, int N, const Branches& br = kOneSolve, int map = kMapGrid) {
+#define X(l, t)                                                                     \
+    if (L == l && T == t) {                                                         \
+        set_lds(line_inv_kernel<l, t>, lds);                                        \
+        line_inv_kernel<l, t><<<g, kThreads, lds, s>>>(spec, dst, twM, N, br, map); \
+        return 0;                                                                   \
     }
     ADMM_LT_CASES(X)
 #undef X
@@ -118,12 +120,13 @@ int launch_team512(hipStream_t s, const float2* first, float2* spec0, float2* sp
     return 0;
 }
 
+// planes: per branch; ngb: plane groups per branch (grid y = branches x ngb), 0: one branch
 int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* so, float* sn,
-                 const float* fmap, float* part, const float2* twM, int N, int planes, int G, int sz) {
+                 const float* fmap, float* part, const float2* twM, int N, int planes, int G, int sz, int ngb = 0) {
 #define X(l, t)                                                                                             \
     if (L == l && T == t) {                                                                                 \
         set_lds(iso_a_kernel<l, t>, lds);                                                                   \
-        iso_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, so, sn, fmap, part, twM, N, planes, G, sz);     \
+        iso_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, so, sn, fmap, part, twM, N, planes, G, sz, ngb); \
         return 0;                                                                                           \
     }
     ADMM_LT_CASES(X)
@@ -132,11 +135,12 @@ int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* 
 }
 
 int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* sn, const float* fmap,
-                 const float* hty, float2* spec0, const float2* twM, int N, const float* prm) {
+                 const float* hty, float2* spec0, const float2* twM, int N, const float* prm,
+                 const Branches& br = kOneSolve) {
 #define X(l, t)                                                                               \
     if (L == l && T == t) {                                                                   \
         set_lds(iso_b_kernel<l, t>, lds);                                                     \
-        iso_b_kernel<l, t><<<g, kThreads, lds, s>>>(sn, fmap, hty, spec0, twM, N, prm);      \
+        iso_b_kernel<l, t><<<g, kThreads, lds, s>>>(sn, fmap, hty, spec0, twM, N, prm, br);  \
         return 0;                                                                             \
     }
     ADMM_LT_CASES(X)
@@ -146,12 +150,13 @@ int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* s
 
 template <int MUL, bool SAVE, bool ACCQ>
 int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst, const float* C,
-                    const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, double* Qp) {
+                    const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, double* Qp,
+                    const Branches& br) {
     const int nt = column_threads(N);
 #define X(v)                                                                                                   \
     if (N == v && nt == kThreads) {                                                                            \
         set_lds(column_kernel<v, MUL, SAVE, ACCQ>, lds);                                                       \
-        column_kernel<v, MUL, SAVE, ACCQ><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \
+        column_kernel<v, MUL, SAVE, ACCQ><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
         return 0;                                                                                              \
     }
     ADMM_N_CASES(X)
@@ -159,7 +164,7 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
 #define X(v)                                                                                                   \
     if (N == v && nt == 512) {                                                                                 \
         set_lds(column_kernel<v, MUL, SAVE, ACCQ, 512>, lds);                                                  \
-        column_kernel<v, MUL, SAVE, ACCQ, 512><<<g, 512, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp);  \
+        column_kernel<v, MUL, SAVE, ACCQ, 512><<<g, 512, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
         return 0;                                                                                              \
     }
     X(256) X(512) X(1024)
@@ -167,7 +172,7 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
 #define X(v)                                                                                                   \
     if (N == v && nt == 1024) {                                                                                \
         set_lds(column_kernel<v, MUL, SAVE, ACCQ, 1024>, lds);                                                 \
-        column_kernel<v, MUL, SAVE, ACCQ, 1024><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp); \
+        column_kernel<v, MUL, SAVE, ACCQ, 1024><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
         return 0;                                                                                              \
     }
     X(256) X(512) X(1024)
@@ -175,16 +180,17 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
     return -1;
 }
 
-// mode: 0 = x-update C, 1 = conj(Sigma_c) (H^T), 2 = Sigma_c (H), 3 = C + save spectrum, 4 = C + accumulate Q
+// mode: 0 = x-update C, 1 = conj(Sigma_c) (H^T), 2 = Sigma_c (H), 3 = C + save spectrum, 4 = C + accumulate Q;
+// br: several branches (C per branch, br.tab_f floats apart)
 int launch_column(int N, int mode, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
                   const float* C, const float2* G, const float2* twN, int L, int KB, float cs,
-                  float2* vsave = nullptr, double* Qp = nullptr) {
+                  float2* vsave = nullptr, double* Qp = nullptr, const Branches& br = kOneSolve) {
     switch (mode) {
-        case 0: return launch_column_t<0, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
-        case 1: return launch_column_t<1, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
-        case 2: return launch_column_t<2, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
-        case 3: return launch_column_t<0, true, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
-        case 4: return launch_column_t<0, false, true>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp);
+        case 0: return launch_column_t<0, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
+        case 1: return launch_column_t<1, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
+        case 2: return launch_column_t<2, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
+        case 3: return launch_column_t<0, true, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
+        case 4: return launch_column_t<0, false, true>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
     }
     return -1;
 }
@@ -669,16 +675,18 @@ int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
     return -1;
 }
 
+// br / ngb / pbs: several branches (planes per branch, plane groups per branch, doubles between the branches'
+// partial-row blocks)
 int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
                      const float* sk, const float* xK, const float* nrm1, const float* sb_in, float* wbar, float* vsum,
                      float* rpartial, double* part, const float2* twM, int N, int planes, int G, const float* prm,
-                     int first_k, int last_k) {
+                     int first_k, int last_k, const Branches& br = kOneSolve, int ngb = 0, size_t pbs = 0) {
 #define X(l, t)                                                                                                 \
     if (L == l && T == t) {                                                                                     \
         set_lds(iso_adj_a_kernel<l, t>, lds);                                                                   \
         iso_adj_a_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, nrm1, nullptr, sb_in, wbar, vsum,  \
                                                          rpartial, part, twM, N, planes, G, prm, first_k,  \
-                                                         last_k);                                               \
+                                                         last_k, br, ngb, pbs);                                 \
         return 0;                                                                                               \
     }
     ADMM_LT_CASES(X)
@@ -688,12 +696,12 @@ int launch_iso_adj_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const floa
 
 int launch_iso_adj_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* wbar, const float* sb_in,
                      const float* sk1, const float* nrm1, const float* Rmap, float* sb_out, float2* spec0,
-                     const float2* twM, int N, const float* prm) {
+                     const float2* twM, int N, const float* prm, const Branches& br = kOneSolve) {
 #define X(l, t)                                                                                                 \
     if (L == l && T == t) {                                                                                     \
         set_lds(iso_adj_b_kernel<l, t>, lds);                                                                   \
         iso_adj_b_kernel<l, t><<<g, kThreads, lds, s>>>(wbar, sb_in, sk1, nrm1, Rmap, sb_out, spec0, twM, N,    \
-                                                         prm);                                                  \
+                                                         prm, br);                                              \
         return 0;                                                                                               \
     }
     ADMM_LT_CASES(X)
@@ -1020,6 +1028,144 @@ int launch_backward(int phases, const float* y, const float* x_bar, float* y_bar
     return ln.finish();
 }
 
+// ---- several isotropic branches below the plane-count rule: the 2-pass kernels over every branch's planes ----
+// Grid plane q = i ppb + loc is branch i's solve of input plane loc (y shared, x_out / x_bar in the chcat layout:
+// the line transforms map planes, admm_kernels.hip PlaneMap); per branch its C table, {tau, rho, lambda}, f map,
+// |s| slots, R map and plane groups.  The step sequence is run_forward's / launch_backward's 2-pass isotropic one.
+Branches multi2_branches(int P, int B, int nbr) { return Branches{P * B, nbr, P, (unsigned)(multi_C_bytes() / 4), 4u}; }
+
+int run_multi_2pass_iso_fwd(Launcher& ln, const float* y, float* x_out, int P, int B, int nbr, int maxit, bool rec,
+                            unsigned char* ws, size_t planes, const MultiLayout& Ly) {
+    hipStream_t s = ln.s;
+    constexpr int M = kMultiM, N = kMultiN, L = M / 2;
+    const size_t MN = (size_t)M * N, ppb = (size_t)P * B, sstride = planes * 2 * MN;
+    const Branches br = multi2_branches(P, B, nbr);
+    const int T = line_T(M, N), KB = column_KB(M, N);
+    const size_t flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
+    float2* twM = reinterpret_cast<float2*>(ws + Ly.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + Ly.twN);
+    const float* Ct = reinterpret_cast<const float*>(ws + Ly.C);
+    const float* prm = reinterpret_cast<const float*>(ws + Ly.prm);
+    float2* spec0 = reinterpret_cast<float2*>(ws + Ly.spec0);
+    float2* spec1 = reinterpret_cast<float2*>(ws + Ly.spec1);
+    float* fmap = reinterpret_cast<float*>(ws + Ly.fmap);
+    float* qpart = reinterpret_cast<float*>(ws + Ly.qpart);
+    float* traj = rec ? reinterpret_cast<float*>(ws + Ly.traj) : nullptr;
+    float* nrm = rec ? reinterpret_cast<float*>(ws + Ly.nrm) : nullptr;
+    float* sA = rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sA);
+    int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N, br, kMapIn); });
+    if (rc) return rc;
+    for (int it = 1; it <= maxit; ++it) {
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            return launch_column(N, 0, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+        });
+        if (rc) return rc;
+        if (it == maxit) {
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N, br, kMapOut); });
+            if (rc) return rc;
+            break;
+        }
+        // recording: s_it into slot it - 1 (the first iteration reads no s), |s_it| into norm slot it - 1
+        float* sn = rec ? traj + (size_t)(it - 1) * sstride : sA;
+        const float* so = rec ? (it >= 2 ? traj + (size_t)(it - 2) * sstride : sn) : sA;
+        float* nrm_out = rec ? nrm + (size_t)(it - 1) * nbr * MN : nullptr;
+        rc = ln.run(ADMM_K_LINE, [&] {
+            return launch_iso_a(L, T, dim3(N / T, (unsigned)(nbr * Ly.ngb)), iso_a_lds(M, T), s, spec1, so, sn, fmap,
+                                qpart, twM, N, (int)ppb, Ly.G, it == 1 ? 1 : 0, Ly.ngb);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_NORM, [&] {
+            hipLaunchKernelGGL(admm::iso_r_kernel, dim3((unsigned)std::min<size_t>((MN + 63) / 64, 2048), (unsigned)nbr),
+                               dim3(kThreads), 0, s, qpart, fmap, Ly.ngb, MN, prm, nrm_out, 4u);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_LINE, [&] {
+            return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, y, spec0, twM, N, prm, br);
+        });
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
+int run_multi_2pass_iso_bwd(Launcher& ln, const float* x_bar, float* y_bar, float* lambda_bar, int P, int B, int nbr,
+                            int K, unsigned char* ws, size_t planes, const MultiLayout& Ly) {
+    hipStream_t s = ln.s;
+    constexpr int M = kMultiM, N = kMultiN, L = M / 2;
+    const size_t MN = (size_t)M * N, ppb = (size_t)P * B, sstride = planes * 2 * MN;
+    const Branches br = multi2_branches(P, B, nbr);
+    const int T = bwd_line_T(M, N, true), KB = column_KB(M, N);
+    const size_t flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
+    float2* twM = reinterpret_cast<float2*>(ws + Ly.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + Ly.twN);
+    const float* Ct = reinterpret_cast<const float*>(ws + Ly.C);
+    const float* prm = reinterpret_cast<const float*>(ws + Ly.prm);
+    float2* specA = reinterpret_cast<float2*>(ws + Ly.spec0);
+    float2* specB = reinterpret_cast<float2*>(ws + Ly.spec1);
+    const float* traj = reinterpret_cast<const float*>(ws + Ly.traj);
+    const float* nrm = reinterpret_cast<const float*>(ws + Ly.nrm);
+    float* sb[2] = {reinterpret_cast<float*>(ws + Ly.sbA), reinterpret_cast<float*>(ws + Ly.sbB)};
+    float* vsum = y_bar ? reinterpret_cast<float*>(ws + Ly.vsum) : nullptr;
+    float* wbar = reinterpret_cast<float*>(ws + Ly.wbar);
+    float* Rmap = reinterpret_cast<float*>(ws + Ly.rmap);
+    float* Rpart = reinterpret_cast<float*>(ws + Ly.Rpart);
+    double* part = reinterpret_cast<double*>(ws + Ly.part);
+    hipError_t e = hipMemsetAsync(part, 0, (size_t)nbr * Ly.pbs * 8, s);   // k = 1 launches no ISO_ADJ_R
+    if (e == hipSuccess && vsum) e = hipMemsetAsync(vsum, 0, planes * MN * 4, s);
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N, br, kMapOut); });
+    if (rc) return rc;
+    for (int k = K; k >= 1; --k) {
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            return launch_column(N, 0, gc, clds, s, specA, specB, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+        });
+        if (rc) return rc;
+        const float* sk1 = k >= 2 ? traj + (size_t)(k - 2) * sstride : nullptr;
+        const float* sbi = k < K ? sb[k & 1] : nullptr;
+        float* sbo = sb[(k & 1) ^ 1];
+        double* rp = part + (size_t)(K - k) * Ly.rows_b * 2;
+        const float* nrm1 = k >= 2 ? nrm + (size_t)(k - 2) * nbr * MN : nullptr;
+        rc = ln.run(ADMM_K_ADJ, [&] {
+            return launch_iso_adj_a(L, T, dim3(N / T, (unsigned)(nbr * Ly.ngb)), iso_a_lds(M, T) + 8 * 16, s, specB, sk1,
+                                    nullptr, nullptr, nrm1, sbi, wbar, vsum, Rpart, rp, twM, N, (int)ppb, Ly.G, prm,
+                                    k == 1 ? 1 : 0, k == K ? 1 : 0, br, Ly.ngb, Ly.pbs);
+        });
+        if (rc) return rc;
+        if (k == 1) break;
+        rc = ln.run(ADMM_K_NORM, [&] {
+            hipLaunchKernelGGL(admm::iso_adj_r_kernel, dim3(kIsoAdjRBlocks, (unsigned)nbr), dim3(kThreads), 0, s, Rpart,
+                               Rmap, nrm1, Ly.ngb, MN, prm, rp + (size_t)Ly.nblk_a * 2, 4u, Ly.pbs);
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_ADJ, [&] {
+            return launch_iso_adj_b(L, T, gl, iso_b_lds(M, T), s, wbar, sbi, sk1, nrm1, Rmap, sbo, specA, twM, N, prm, br);
+        });
+        if (rc) return rc;
+    }
+    double* rt = reinterpret_cast<double*>(ws + Ly.rt);
+    for (int i = 0; i < nbr; ++i) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            launch_reduce_cols(s, part + (size_t)i * Ly.pbs, rt + 2 * i, K * Ly.rows_b, 2,
+                               reinterpret_cast<double*>(ws + Ly.rtmp));
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::grads_final_kernel, dim3(1), dim3(64), 0, s, rt + 2 * i, (const double*)nullptr,
+                               (const double*)nullptr, 0, prm + 4 * i, lambda_bar ? lambda_bar + i : nullptr,
+                               (float*)nullptr, (float*)nullptr);
+        });
+        if (rc) return rc;
+    }
+    if (y_bar) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::branch_sum_kernel, dim3(1024), dim3(kThreads), 0, s, vsum, y_bar, ppb * MN, nbr);
+        });
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
 int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int B, int nbr, const float* const* lambda,
                          const float* const* rho, int maxit, int flags, void* workspace, void* stream, size_t planes,
                          const MultiLayout& L) {
@@ -1042,6 +1188,7 @@ int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int 
                                (float2*)nullptr, (const float*)nullptr, 0, 0, M, N, sc, prm + 4 * i, (double2*)nullptr);
         });
         if (rc) return rc;
+        if (L.two_pass) continue;   // the 2-pass kernels read Ct itself
         rc = ln.run(ADMM_K_SETUP, [&] { return admm::plane::launch_tables(Ct, nullptr, F, s); });
         if (rc) return rc;
     }
@@ -1050,8 +1197,13 @@ int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int 
         if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
         return ln.finish();
     }
-    const admm::plane::Branches br = multi_branches(P, B, nbr);
     const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = rec && (flags & ADMM_REC_MASKS) != 0;
+    if (L.two_pass) {
+        rc = run_multi_2pass_iso_fwd(ln, y, x_out, P, B, nbr, maxit, rec, ws, planes, L);
+        if (rc) return rc;
+        return ln.finish();
+    }
+    const admm::plane::Branches br = multi_branches(P, B, nbr);
     if (flags & ADMM_MULTI_ISO) {
         // isotropic: per iteration one plane256_iso_kernel over every branch's planes and one iso_norm_kernel
         // (each branch's batch norm over its own planes); recording: s_{k+1} into slot k, |s_{k+1}| too
@@ -1100,6 +1252,11 @@ int launch_backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, f
         if (y_bar && (e = hipMemsetAsync(y_bar, 0, ppb * MN * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
         if (lambda_bar && (e = hipMemsetAsync(lambda_bar, 0, (size_t)nbr * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
         if (rho_bar && (e = hipMemsetAsync(rho_bar, 0, (size_t)nbr * 4, s)) != hipSuccess) return fail(ADMM_E_HIP, "memset");
+        return ln.finish();
+    }
+    if (L.two_pass) {
+        rc = run_multi_2pass_iso_bwd(ln, x_bar, y_bar, lambda_bar, P, B, nbr, K, ws, planes, L);
+        if (rc) return rc;
         return ln.finish();
     }
     const admm::plane::Branches br = multi_branches(P, B, nbr);

@@ -26,6 +26,19 @@ struct Branches {
     unsigned tab_f;   // floats between the branches' lane-native table blocks (tables_bytes() / 4)
     unsigned prm_f;   // floats between the branches' {tau, rho, lambda} blocks
 };
+// Where grid plane q reads and writes (above).  The 2-pass kernels (admm_kernels.hip) take the same struct, with
+// tab_f = floats between the branches' 2-pass C tables.
+struct BranchOf {
+    int i;
+    size_t in_plane, out_plane;
+};
+__host__ __device__ inline BranchOf branch_of(const Branches& br, size_t plane) {
+    if (br.nbr == 1) return {0, plane, plane};
+    const int i = (int)(plane / (size_t)br.ppb);
+    const size_t loc = plane - (size_t)i * br.ppb;
+    const size_t b = loc / (size_t)br.P, p = loc - b * br.P;
+    return {i, loc, (b * br.nbr + i) * br.P + p};
+}
 constexpr int kTabEntries = 2 * 32 * 512;   // lane-native spectral table entries (= 256 x 128)
 
 // bytes of the lane-native tables (Cf, C0b, Gf, G0b) carved from the workspace

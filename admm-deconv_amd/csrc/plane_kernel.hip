@@ -87,19 +87,6 @@ __device__ __forceinline__ void bstu(rsrc_t r, unsigned vo, unsigned so, unsigne
     __builtin_amdgcn_raw_buffer_store_b32(v, r, vo, so, 0);
 }
 
-// Branches (plane_api.hpp): plane q of the grid is plane q % ppb of the shared input, run with branch
-// i = q / ppb's tables and scalars, its output at the chcat position of branch i (image b, channel i P + p).
-struct BranchOf {
-    int i;
-    size_t in_plane, out_plane;
-};
-__device__ __forceinline__ BranchOf branch_of(const Branches& br, size_t plane) {
-    if (br.nbr == 1) return {0, plane, plane};
-    const int i = (int)(plane / (size_t)br.ppb);
-    const size_t loc = plane - (size_t)i * br.ppb;
-    const size_t b = loc / (size_t)br.P, p = loc - b * br.P;
-    return {i, loc, (b * br.nbr + i) * br.P + p};
-}
 
 // Mask-bit trajectory (record mode 2: the reverse sweep will not form rho_bar, so it needs only the ST
 // branch of every s_k element, not s_k itself).  Per element c of a lane's register n (float4 (s1, s1', s2,

@@ -93,9 +93,10 @@ def test_recorded_gradients_both_sides_of_the_plane_rule(dev):
 
 
 def test_merged_branches_vs_per_branch_at_the_default_rule(dev):
-    """Parallel's merged isotropic grid (fused kernels over all 5 branches' planes) against
-    the branches one by one, each small enough (3 planes) for the 2-pass isotropic kernels at the default rule:
-    the same solves through different paths agree to fp32 rounding (rel-L2 <= 2e-5 per plane), not bitwise."""
+    """Parallel's merged isotropic grid against the branches one by one at the default rule.
+    Both sides are below it (9 planes merged, 3 per branch), so both run the 2-pass isotropic kernels (the merged
+    grid over all branches' planes, round 5): bitwise the same.  The merged grid through the per-plane kernels
+    (MIN_PLANES = 0) agrees to fp32 rounding (rel-L2 <= 2e-5 per plane)."""
     rng = np.random.default_rng(0)
     branch = [layers.ADMMDeconvF2((), 8, r, layers.relu1, iso=True, rng=rng, device=dev) for r in (0.02, 0.2, 2.0)]
     x = torch.from_numpy(synth.make_batch(1, 256, 256, None, P=3, sigma=0.1)).to(dev)
@@ -103,8 +104,12 @@ def test_merged_branches_vs_per_branch_at_the_default_rule(dev):
     assert merged._mergeable(x)
     assert _lib.query_paths(256, 256, True, 0, planes=3)[0] == "2pass_iso"
     with torch.no_grad():
-        a = merged(x).cpu().numpy().astype(np.float64)
-        b = layers.Parallel(layers.chcat, *branch, merge=False)(x).cpu().numpy().astype(np.float64)
+        a = merged(x)
+        b = layers.Parallel(layers.chcat, *branch, merge=False)(x)
+        assert torch.equal(a, b)
+        with _lib.option("MIN_PLANES", 0):
+            b = merged(x)
+    a, b = a.cpu().numpy().astype(np.float64), b.cpu().numpy().astype(np.float64)
     a, b = a.reshape(-1, 256 * 256), b.reshape(-1, 256 * 256)
     nz = np.linalg.norm(b, axis=1) > 0
     rel = np.linalg.norm(a - b, axis=1)[nz] / np.linalg.norm(b, axis=1)[nz]

@@ -4,7 +4,7 @@ import pytest
 import torch
 
 import oracle_np
-from admm_deconv import layers, synth
+from admm_deconv import _lib, layers, synth
 from parity import assert_parity, assert_parity_fp32ref
 
 pytestmark = pytest.mark.gpu
@@ -131,15 +131,20 @@ def test_parallel_branches_on_streams_match_serial(dev, train_rho, iso):
             assert all(torch.equal(a, b) for a, b in zip(r1, r2))
 
 
-@pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])
+@pytest.mark.parametrize("iso", [False, True, pytest.param("rule", marks=pytest.mark.min_planes_rule)],
+                         ids=["aniso", "iso", "iso-default-rule"])
 def test_c5_denoiser_branch_gradients(dev, iso):
     """BASELINE c5's caller: the get_denoiser branch of src/nets/net_build.jl:113-128 -- Parallel(chcat) of
     5 x ADMMDeconvF2((), 50, rho, relu1, iso=use_iso) -- on a small RGB batch (2 x 3 planes of 256^2),
-    branches on their own HIP streams; iso = true is the training default (src/configs/train_cfg.json:14),
+    branches in one grid; iso = true is the training default (src/configs/train_cfg.json:14),
     where the batch norm couples the 6 planes of a branch.  The gradient of a weighted sum of the output
     w.r.t. every branch's trainable lambda (deconv_admm.jl:107) against fp64 autograd of the oracle: for
-    branch i, lambda_bar = <xbar_i, d x_i / d lambda> with xbar_i = w_i * relu1'(x_i)."""
+    branch i, lambda_bar = <xbar_i, d x_i / d lambda> with xbar_i = w_i * relu1'(x_i).  iso-default-rule: the
+    library's plane-count rule at its default, under which these 30 planes run the 2-pass kernels over all five
+    branches in one grid (the reference's training configuration, train_cfg.json:10-14)."""
     import oracle_torch
+    rule = iso == "rule"
+    iso = bool(iso)
     rng = np.random.default_rng(12)
     rhos = (0.002, 0.02, 0.2, 2.0, 4.0)
     br = [layers.ADMMDeconvF2((), 50, r, layers.relu1, iso=iso, rng=rng, device=dev) for r in rhos]
@@ -148,9 +153,17 @@ def test_c5_denoiser_branch_gradients(dev, iso):
     net = layers.Parallel(layers.chcat, *br)
     y = synth.make_batch(2, 256, 256, None, P=3, sigma=0.1, g0=9)
     w = rng.standard_normal((2, 15, 256, 256)).astype(np.float32)
-    out = net(torch.from_numpy(y).to(dev))
-    (out * torch.from_numpy(w).to(dev)).sum().backward()
-    torch.cuda.synchronize()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    try:
+        out = net(torch.from_numpy(y).to(dev))
+        (out * torch.from_numpy(w).to(dev)).sum().backward()
+        torch.cuda.synchronize()
+        columns = _lib.profile_get(_lib.K_COLUMN)[1]
+    finally:
+        _lib.profile_enable(False)
+    # the merged grid: per-plane kernels (no column launches) with MIN_PLANES = 0, the 2-pass ones at the rule
+    assert (columns > 0) == rule, columns
     for i, (L, r) in enumerate(zip(br, rhos)):
         lam = float(L.lam.detach().cpu()[0])
         x0 = oracle_torch.tvd_fft_torch(torch.from_numpy(y.astype(np.float64)),

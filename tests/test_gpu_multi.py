@@ -153,6 +153,43 @@ def test_multi_iso_is_the_branches(dev, n, B, P, K):
     assert torch.allclose(yb, yb_sum, rtol=1e-6, atol=1e-6 * float(yb_sum.abs().max()))
 
 
+@pytest.mark.min_planes_rule
+@pytest.mark.parametrize("n,B,P,K", [(5, 2, 3, 12), (2, 1, 1, 1), (3, 3, 1, 2), (4, 5, 3, 6)])
+def test_multi_iso_2pass_is_the_branches(dev, n, B, P, K):
+    """Below the plane-count rule (ADMM_OPT_MIN_PLANES at its default; 111 planes in all or fewer) the merged
+    isotropic grid runs the 2-pass kernels over every branch's planes (admm_launch.hip run_multi_2pass_iso_fwd /
+    _bwd, the reference's training configuration: 5 branches x batch 2 x RGB, train_cfg.json:10-14).  Each branch
+    alone is below the rule too, so it runs the same kernels: forward bitwise, lambda_bar to the fp64 order of its
+    partial rows (the rows are laid out per branch), y_bar the branches' sum to rounding."""
+    assert _lib.get_option("MIN_PLANES") == -1 and n * B * P < 112
+    y = torch.from_numpy(synth.make_batch(B, 256, 256, None, P=P, sigma=0.1, g0=4)).to(dev)
+    lams, rhos = _branch_scalars(dev, n, seed=13)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    try:
+        xp = admm_deconv.tvd_fft_multi(y, lams, rhos, K, isotropic=True)
+        columns = _lib.profile_get(_lib.K_COLUMN)[1]
+    finally:
+        _lib.profile_enable(False)
+    assert columns == K, columns   # one column pass per iteration: the 2-pass kernels, one grid for all branches
+    xb = torch.randn((B, n * P, 256, 256), device=dev)
+    x, rec = admm_deconv.tvd_fft_multi(y, lams, rhos, K, record=True, need_rho=False, isotropic=True)
+    yb, lb, rb = admm_deconv.tvd_fft_multi_backward_recorded(rec, x, xb, need_rho=False)
+    yb_sum = torch.zeros_like(y)
+    for i in range(n):
+        xi, reci = admm_deconv.tvd_fft_record(y, lams[i], rhos[i], None, True, K, need_rho=False)
+        ybi, _, lbi, _ = admm_deconv.tvd_fft_backward_recorded(reci, xi, xb[:, i * P:(i + 1) * P].contiguous(),
+                                                               need_rho=False)
+        torch.cuda.synchronize()
+        assert torch.equal(xi, x[:, i * P:(i + 1) * P]), i
+        a, b = float(lbi), float(lb[i])
+        assert abs(a - b) <= 1e-6 * abs(a) + 1e-30, (i, a, b)
+        yb_sum += ybi
+    torch.cuda.synchronize()
+    assert rb is None and torch.equal(x, xp)
+    assert torch.allclose(yb, yb_sum, rtol=1e-6, atol=1e-6 * float(yb_sum.abs().max()))
+
+
 def test_multi_iso_vs_oracle_and_refusals(dev):
     y = synth.make_batch(2, 256, 256, None, P=3, sigma=0.1, g0=8)
     lams, rhos = _branch_scalars(dev, 3, seed=2)
