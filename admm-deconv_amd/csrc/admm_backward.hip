@@ -82,8 +82,9 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
                                                             float* __restrict__ vsum, float2* __restrict__ spec0,
                                                             double* __restrict__ part, const float2* __restrict__ twM,
                                                             int N, const float* __restrict__ prm, int first_k /*k==1*/,
-                                                            int last_k /*k==K*/) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
+                                                            int last_k /*k==K*/, Branches br = kOneSolve, size_t pbs = 0) {
+    // several branches (admm_kernels.hip Branches): own scalars, x_K in the chcat layout, the partial rows of
+    // branch i pbs doubles on, rows by the plane's index within its branch
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -102,6 +103,8 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
     const size_t MN = (size_t)M * N;
     const int tid = threadIdx.x;
     const size_t poff = (size_t)plane * 2 * MN;
+    const BranchOf bo = branch_of(br, plane);
+    const float tau = prm[(size_t)bo.i * br.prm_f], rho = prm[(size_t)bo.i * br.prm_f + 1];   // (setup_kernel)
 
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     load_lines<L>(spec1 + (size_t)plane * N * L, X, j0 - 1, TH, N);
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
             // ---- rho_bar: -<Dvb, D x_k> (xK / sk null: rho_bar not wanted, no reads) ----
             float dx0[4] = {0, 0, 0, 0}, dx1[4] = {0, 0, 0, 0};
             if (last_k && xK) {
-                const float* xp = xK + (size_t)plane * MN;
+                const float* xp = xK + bo.out_plane * MN;
                 const float4 xc = *reinterpret_cast<const float4*>(xp + off);
                 const float4 xq = *reinterpret_cast<const float4*>(xp + (size_t)((j0 + t - 1) & (N - 1)) * M + i);
                 const float xl = xp[(size_t)((j0 + t) & (N - 1)) * M + ((i - 1) & (M - 1))];
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void line_adj_kernel(const float2* __rest
             }
         }
     }
-    block_sum2(rho_acc, tau_acc, part + 2 * ((size_t)plane * gridDim.x + xb.x), red);
+    block_sum2(rho_acc, tau_acc, part + (size_t)bo.i * pbs + 2 * (bo.in_plane * gridDim.x + xb.x), red);
     if (first_k) return;   // k = 1: no g_0 (block-uniform)
     __syncthreads();
     // ---- g_{k-1} = D^T sbar_{k-1}, fed straight into the forward pass 0 along dim 1 ----

@@ -298,31 +298,41 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
     L.C = take((size_t)nbr * multi_C_bytes());
     L.two_pass = multi_two_pass(planes, flags);
     if (L.two_pass) {
-        // the 2-pass isotropic kernels over every branch's planes (admm_launch.hip run_multi_2pass_iso_*)
+        // the 2-pass kernels over every branch's planes (admm_launch.hip run_multi_2pass_*)
         const size_t ppb = planes / (size_t)nbr;
-        L.G = iso_group(ppb);
-        L.ngb = iso_ngroups(ppb);
-        L.nblk_a = L.ngb * (kMultiN / bwd_line_T(kMultiM, kMultiN, true));
-        L.rows_b = L.nblk_a + kIsoAdjRBlocks;
+        const int T = bwd_line_T(kMultiM, kMultiN, iso);
+        if (iso) {
+            L.G = iso_group(ppb);
+            L.ngb = iso_ngroups(ppb);
+            L.nblk_a = L.ngb * (kMultiN / T);
+            L.rows_b = L.nblk_a + kIsoAdjRBlocks;
+        } else {
+            L.rows_b = (int)ppb * (kMultiN / T);
+        }
         L.pbs = (size_t)K * L.rows_b * 2;
         L.spec0 = take(planes * MN * 4);
         L.spec1 = take(planes * MN * 4);
-        L.fmap = take((size_t)nbr * MN * 4);
-        L.qpart = take((size_t)nbr * L.ngb * MN * 4);
+        if (iso) {
+            L.fmap = take((size_t)nbr * MN * 4);
+            L.qpart = take((size_t)nbr * L.ngb * MN * 4);
+        }
         if (rec) {
             L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * MN * 8);
-            L.nrm = take((size_t)(K > 1 ? K - 1 : 1) * nbr * MN * 4);
             L.sbA = take(planes * MN * 8);
             L.sbB = take(planes * MN * 8);
             L.vsum = take(planes * MN * 4);
-            L.wbar = take(planes * MN * 4);
-            L.rmap = take((size_t)nbr * MN * 4);
-            L.Rpart = take((size_t)nbr * L.ngb * MN * 4);
             L.part = take((size_t)nbr * L.pbs * 8);
             L.rt = take((size_t)nbr * 16);
             L.rtmp = take((size_t)kRedParts * 2 * 8);
+            if (iso) {
+                L.nrm = take((size_t)(K > 1 ? K - 1 : 1) * nbr * MN * 4);
+                L.wbar = take(planes * MN * 4);
+                L.rmap = take((size_t)nbr * MN * 4);
+                L.Rpart = take((size_t)nbr * L.ngb * MN * 4);
+            }
         } else {
             L.sA = take(planes * MN * 8);
+            if (!iso) L.sbA = take(planes * MN * 8);   // the anisotropic s ping-pong's second buffer
         }
         L.total = off;
         return L;

@@ -500,8 +500,7 @@ template <int L, int T, int NT = kThreads>
 __device__ __forceinline__ void line_body(XBlk xb, const float2* __restrict__ spec1, float2* __restrict__ spec0,
                                           const float* __restrict__ s_old, float* __restrict__ s_new,
                                           const float* __restrict__ hty, const float2* __restrict__ twM, int N,
-                                          const float* __restrict__ prm, int s_zero) {
-    const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
+                                          const float* __restrict__ prm, int s_zero, Branches br = kOneSolve) {
     constexpr int M = 2 * L;
     constexpr int M4 = M / 4;
     constexpr int TH = T + 2;
@@ -522,7 +521,9 @@ __device__ __forceinline__ void line_body(XBlk xb, const float2* __restrict__ sp
     const int tid = threadIdx.x;
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
-    const float* hp = hty + (size_t)plane * MN;
+    const BranchOf bo = branch_of(br, plane);   // several branches: H^T y = the shared input plane, own scalars
+    const float* hp = hty + bo.in_plane * MN;
+    const float tau = prm[(size_t)bo.i * br.prm_f], rho = prm[(size_t)bo.i * br.prm_f + 1];   // (setup_kernel)
 
     // ---- issue every global load of the block up front -- except at 512-point lines (kJit): there the
     // s / H^T y loads go just before their use, which cuts the registers held across the irFFT (156 -> 88
@@ -683,8 +684,8 @@ template <int L, int T, int NT = kThreads>
 __global__ __launch_bounds__(NT) void line_kernel(const float2* __restrict__ spec1, float2* __restrict__ spec0,
                                                   const float* __restrict__ s_old, float* __restrict__ s_new,
                                                   const float* __restrict__ hty, const float2* __restrict__ twM, int N,
-                                                  const float* __restrict__ prm, int s_zero) {
-    line_body<L, T, NT>(xcd_block(), spec1, spec0, s_old, s_new, hty, twM, N, prm, s_zero);
+                                                  const float* __restrict__ prm, int s_zero, Branches br = kOneSolve) {
+    line_body<L, T, NT>(xcd_block(), spec1, spec0, s_old, s_new, hty, twM, N, prm, s_zero, br);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -69,12 +69,12 @@ int launch_line_inv(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
 
 int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, float2* spec0,
                 const float* so, float* sn, const float* hty, const float2* twM, int N, const float* prm,
-                int sz, int nt = kThreads) {
+                int sz, int nt = kThreads, const Branches& br = kOneSolve) {
     if (nt != kThreads) {   // wider blocks at 512-point lines (update kernel, line_T_upd)
 #define X(l, t, n)                                                                                       \
         if (L == l && T == t && nt == n) {                                                               \
             set_lds(line_kernel<l, t, n>, lds);                                                          \
-            line_kernel<l, t, n><<<g, n, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz);         \
+            line_kernel<l, t, n><<<g, n, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz, br);     \
             return 0;                                                                                    \
         }
         X(256, 8, 512) X(256, 16, 1024) X(256, 4, 512) X(256, 8, 1024)
@@ -84,7 +84,7 @@ int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* s
 #define X(l, t)                                                                                          \
     if (L == l && T == t) {                                                                              \
         set_lds(line_kernel<l, t>, lds);                                                                 \
-        line_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz);    \
+        line_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, spec0, so, sn, hty, twM, N, prm, sz, br); \
         return 0;                                                                                        \
     }
     ADMM_LT_CASES(X)
@@ -650,7 +650,8 @@ void launch_reduce_cols(hipStream_t s, const double* part, double* out, int n, i
 
 int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* sk1,
                     const float* sk, const float* xK, const float* sb_in, float* sb_out, float* vsum, float2* spec0,
-                    double* part, const float2* twM, int N, const float* prm, int first_k, int last_k, bool ln) {
+                    double* part, const float2* twM, int N, const float* prm, int first_k, int last_k, bool ln,
+                    const Branches& br = kOneSolve, size_t pbs = 0) {
     if (ln) {   // trajectory in the fused kernel's lane-native layout (M = 256)
 #define X(l, t)                                                                                                \
         if (L == l && T == t) {                                                                                \
@@ -667,7 +668,7 @@ int launch_line_adj(int L, int T, dim3 g, size_t lds, hipStream_t s, const float
     if (L == l && T == t) {                                                                                    \
         set_lds(line_adj_kernel<l, t>, lds);                                                                   \
         line_adj_kernel<l, t><<<g, kThreads, lds, s>>>(spec1, sk1, sk, xK, sb_in, sb_out, vsum, spec0, part, twM, \
-                                                        N, prm, first_k, last_k);                        \
+                                                        N, prm, first_k, last_k, br, pbs);               \
         return 0;                                                                                              \
     }
     ADMM_LT_CASES(X)
@@ -1028,10 +1029,10 @@ int launch_backward(int phases, const float* y, const float* x_bar, float* y_bar
     return ln.finish();
 }
 
-// ---- several isotropic branches below the plane-count rule: the 2-pass kernels over every branch's planes ----
+// ---- several branches below the plane-count rule: the 2-pass kernels over every branch's planes ----
 // Grid plane q = i ppb + loc is branch i's solve of input plane loc (y shared, x_out / x_bar in the chcat layout:
 // the line transforms map planes, admm_kernels.hip PlaneMap); per branch its C table, {tau, rho, lambda}, f map,
-// |s| slots, R map and plane groups.  The step sequence is run_forward's / launch_backward's 2-pass isotropic one.
+// |s| slots, R map and plane groups.  The step sequences are run_forward's / launch_backward's 2-pass ones.
 Branches multi2_branches(int P, int B, int nbr) { return Branches{P * B, nbr, P, (unsigned)(multi_C_bytes() / 4), 4u}; }
 
 int run_multi_2pass_iso_fwd(Launcher& ln, const float* y, float* x_out, int P, int B, int nbr, int maxit, bool rec,
@@ -1166,6 +1167,109 @@ int run_multi_2pass_iso_bwd(Launcher& ln, const float* x_bar, float* y_bar, floa
     return ADMM_OK;
 }
 
+int run_multi_2pass_fwd(Launcher& ln, const float* y, float* x_out, int P, int B, int nbr, int maxit, bool rec,
+                        unsigned char* ws, size_t planes, const MultiLayout& Ly) {
+    hipStream_t s = ln.s;
+    constexpr int M = kMultiM, N = kMultiN, L = M / 2;
+    const size_t MN = (size_t)M * N, sstride = planes * 2 * MN;
+    const Branches br = multi2_branches(P, B, nbr);
+    const int T = line_T(M, N), KB = column_KB(M, N);
+    const size_t llds = line_lds(M, T), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
+    float2* twM = reinterpret_cast<float2*>(ws + Ly.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + Ly.twN);
+    const float* Ct = reinterpret_cast<const float*>(ws + Ly.C);
+    const float* prm = reinterpret_cast<const float*>(ws + Ly.prm);
+    float2* spec0 = reinterpret_cast<float2*>(ws + Ly.spec0);
+    float2* spec1 = reinterpret_cast<float2*>(ws + Ly.spec1);
+    float* traj = rec ? reinterpret_cast<float*>(ws + Ly.traj) : nullptr;
+    float* sbuf[2] = {rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sA), rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sbA)};
+    int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N, br, kMapIn); });
+    if (rc) return rc;
+    for (int it = 1; it <= maxit; ++it) {
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            return launch_column(N, 0, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+        });
+        if (rc) return rc;
+        if (it == maxit) {
+            rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N, br, kMapOut); });
+            if (rc) return rc;
+            break;
+        }
+        // recording: s_it into slot it - 1 (the first iteration reads no s); otherwise the two s buffers in turn
+        float* sn = rec ? traj + (size_t)(it - 1) * sstride : ((it & 1) ? sbuf[0] : sbuf[1]);
+        const float* so = rec ? (it >= 2 ? traj + (size_t)(it - 2) * sstride : sn) : ((it & 1) ? sbuf[1] : sbuf[0]);
+        rc = ln.run(ADMM_K_LINE, [&] {
+            return launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, y, twM, N, prm, it == 1 ? 1 : 0, kThreads, br);
+        });
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
+int run_multi_2pass_bwd(Launcher& ln, const float* x_bar, float* y_bar, float* lambda_bar, float* rho_bar,
+                        const float* x_out, int P, int B, int nbr, int K, unsigned char* ws, size_t planes,
+                        const MultiLayout& Ly) {
+    hipStream_t s = ln.s;
+    constexpr int M = kMultiM, N = kMultiN, L = M / 2;
+    const size_t MN = (size_t)M * N, ppb = (size_t)P * B, sstride = planes * 2 * MN;
+    const Branches br = multi2_branches(P, B, nbr);
+    const int T = bwd_line_T(M, N, false), KB = column_KB(M, N);
+    const size_t alds = line_lds(M, T) + 8 * 16, flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
+    const dim3 gl(N / T, (unsigned)planes), gc(L / KB, (unsigned)planes);
+    float2* twM = reinterpret_cast<float2*>(ws + Ly.twM);
+    float2* twN = reinterpret_cast<float2*>(ws + Ly.twN);
+    const float* Ct = reinterpret_cast<const float*>(ws + Ly.C);
+    const float* prm = reinterpret_cast<const float*>(ws + Ly.prm);
+    float2* specA = reinterpret_cast<float2*>(ws + Ly.spec0);
+    float2* specB = reinterpret_cast<float2*>(ws + Ly.spec1);
+    const float* traj = reinterpret_cast<const float*>(ws + Ly.traj);
+    float* sb[2] = {reinterpret_cast<float*>(ws + Ly.sbA), reinterpret_cast<float*>(ws + Ly.sbB)};
+    float* vsum = y_bar ? reinterpret_cast<float*>(ws + Ly.vsum) : nullptr;
+    double* part = reinterpret_cast<double*>(ws + Ly.part);
+    hipError_t e = vsum ? hipMemsetAsync(vsum, 0, planes * MN * 4, s) : hipSuccess;
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, x_bar, specA, twM, N, br, kMapOut); });
+    if (rc) return rc;
+    for (int k = K; k >= 1; --k) {
+        rc = ln.run(ADMM_K_COLUMN, [&] {
+            return launch_column(N, 0, gc, clds, s, specA, specB, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+        });
+        if (rc) return rc;
+        const float* sk1 = k >= 2 ? traj + (size_t)(k - 2) * sstride : nullptr;
+        const float* skk = k < K ? traj + (size_t)(k - 1) * sstride : nullptr;
+        const float* sbi = k < K ? sb[k & 1] : nullptr;
+        float* sbo = sb[(k & 1) ^ 1];
+        double* rp = part + (size_t)(K - k) * Ly.rows_b * 2;
+        rc = ln.run(ADMM_K_ADJ, [&] {
+            return launch_line_adj(L, T, gl, alds, s, specB, sk1, rho_bar ? skk : nullptr, rho_bar ? x_out : nullptr, sbi,
+                                   sbo, vsum, specA, rp, twM, N, prm, k == 1 ? 1 : 0, k == K ? 1 : 0, false, br, Ly.pbs);
+        });
+        if (rc) return rc;
+    }
+    double* rt = reinterpret_cast<double*>(ws + Ly.rt);
+    for (int i = 0; i < nbr; ++i) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            launch_reduce_cols(s, part + (size_t)i * Ly.pbs, rt + 2 * i, K * Ly.rows_b, 2,
+                               reinterpret_cast<double*>(ws + Ly.rtmp));
+        });
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::grads_final_kernel, dim3(1), dim3(64), 0, s, rt + 2 * i, (const double*)nullptr,
+                               (const double*)nullptr, 0, prm + 4 * i, lambda_bar ? lambda_bar + i : nullptr,
+                               rho_bar ? rho_bar + i : nullptr, (float*)nullptr);
+        });
+        if (rc) return rc;
+    }
+    if (y_bar) {
+        rc = ln.run(ADMM_K_FINAL, [&] {
+            hipLaunchKernelGGL(admm::branch_sum_kernel, dim3(1024), dim3(kThreads), 0, s, vsum, y_bar, ppb * MN, nbr);
+        });
+        if (rc) return rc;
+    }
+    return ADMM_OK;
+}
+
 int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int B, int nbr, const float* const* lambda,
                          const float* const* rho, int maxit, int flags, void* workspace, void* stream, size_t planes,
                          const MultiLayout& L) {
@@ -1199,7 +1303,8 @@ int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int 
     }
     const bool rec = (flags & ADMM_MULTI_RECORD) != 0, masks = rec && (flags & ADMM_REC_MASKS) != 0;
     if (L.two_pass) {
-        rc = run_multi_2pass_iso_fwd(ln, y, x_out, P, B, nbr, maxit, rec, ws, planes, L);
+        rc = (flags & ADMM_MULTI_ISO) ? run_multi_2pass_iso_fwd(ln, y, x_out, P, B, nbr, maxit, rec, ws, planes, L)
+                                      : run_multi_2pass_fwd(ln, y, x_out, P, B, nbr, maxit, rec, ws, planes, L);
         if (rc) return rc;
         return ln.finish();
     }
@@ -1255,7 +1360,9 @@ int launch_backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, f
         return ln.finish();
     }
     if (L.two_pass) {
-        rc = run_multi_2pass_iso_bwd(ln, x_bar, y_bar, lambda_bar, P, B, nbr, K, ws, planes, L);
+        rc = (flags & ADMM_MULTI_ISO)
+                 ? run_multi_2pass_iso_bwd(ln, x_bar, y_bar, lambda_bar, P, B, nbr, K, ws, planes, L)
+                 : run_multi_2pass_bwd(ln, x_bar, y_bar, lambda_bar, rho_bar, x_out, P, B, nbr, K, ws, planes, L);
         if (rc) return rc;
         return ln.finish();
     }

@@ -94,13 +94,13 @@ bool enough_planes(const PathIn& q, MinPlanesFor which) {
     }
     return true;
 }
-// Several isotropic 256 x 256 branches in one grid (admm_tvd_forward_multi_dev_f32): the per-plane split-iteration
-// kernels from kMinFusedIso planes in all, below that the 2-pass kernels over every branch's planes (the c5
-// training step at batch 2 has 30: tools/small_batch_probe.py, profiles/r05_small_batch_probe.jsonl).
+// Several 256 x 256 branches in one grid (admm_tvd_forward_multi_dev_f32): the per-plane kernels from the fused
+// paths' plane counts in all (kMinFused / kMinFusedIso), below them the 2-pass kernels over every branch's planes
+// (the c5 training step at batch 2 has 30: tools/small_batch_probe.py, profiles/r05_small_batch_probe.jsonl).
 bool multi_two_pass(size_t planes, int flags) {
-    if (!(flags & ADMM_MULTI_ISO)) return false;
-    return !enough_planes(PathIn{kMultiM, kMultiN, true, false, ADMM_MODE_FORWARD, 0, false, false, planes},
-                          kMinFusedIso);
+    const bool iso = (flags & ADMM_MULTI_ISO) != 0;
+    return !enough_planes(PathIn{kMultiM, kMultiN, iso, false, ADMM_MODE_FORWARD, 0, false, false, planes},
+                          iso ? kMinFusedIso : kMinFused);
 }
 TrajFlags traj_flags(const PathIn& q, const PathPlan& pl) {
     if (q.mode == ADMM_MODE_FORWARD) return {false, false, false, false, false};

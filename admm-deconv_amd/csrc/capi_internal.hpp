@@ -188,16 +188,17 @@ BwdLayout make_bwd_layout(int M, int N, size_t planes, int kh, int kw, int maxit
 struct MultiLayout {
     size_t prm, twM, twN, C, F, hln, sln, traj, sbar, vsl, part, rt, rtmp, total;
     size_t fmap, qpart, nrm, rmap;   // isotropic (ADMM_MULTI_ISO): f maps, q / R partials, |s| slots, R maps
-    // Below the plane-count rule the isotropic branches run the 2-pass kernels in one grid (multi_two_pass):
-    // spectra, s state, and for the reverse sweep sbar (two), Vsum, vbar and the plane-group R partials; qpart
-    // then holds the plane-group |s|^2 partials, traj / nrm the natural-layout s_k / |s_k| slots (|s_k| per
-    // branch), part the (rho_bar, tau_bar) rows of every branch (pbs doubles apart, rows_b per step)
+    // Below the plane-count rule the branches run the 2-pass kernels in one grid (multi_two_pass): spectra, s
+    // state (anisotropic: sA / sbA ping-pong), and for the reverse sweep sbar (two), Vsum and (isotropic) vbar and
+    // the plane-group R partials; qpart then holds the plane-group |s|^2 partials, traj / nrm the natural-layout
+    // s_k / |s_k| slots (|s_k| per branch), part the (rho_bar, tau_bar) rows of every branch (pbs doubles apart,
+    // rows_b per step)
     bool two_pass;
     size_t spec0, spec1, sA, sbA, sbB, vsum, wbar, Rpart, pbs;
     int ngb, G, rows_b, nblk_a;
 };
 constexpr int kMultiM = 256, kMultiN = 256;
-// several isotropic branches below the fused kernels' plane-count rule run the 2-pass kernels (admm_paths.hip)
+// several branches below the fused kernels' plane-count rule run the 2-pass kernels (admm_paths.hip)
 bool multi_two_pass(size_t planes, int flags);
 size_t multi_C_bytes();
 size_t multi_F_bytes();

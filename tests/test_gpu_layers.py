@@ -131,20 +131,20 @@ def test_parallel_branches_on_streams_match_serial(dev, train_rho, iso):
             assert all(torch.equal(a, b) for a, b in zip(r1, r2))
 
 
-@pytest.mark.parametrize("iso", [False, True, pytest.param("rule", marks=pytest.mark.min_planes_rule)],
-                         ids=["aniso", "iso", "iso-default-rule"])
-def test_c5_denoiser_branch_gradients(dev, iso):
+@pytest.mark.parametrize("iso,rule", [(False, False), (True, False),
+                                      pytest.param(False, True, marks=pytest.mark.min_planes_rule),
+                                      pytest.param(True, True, marks=pytest.mark.min_planes_rule)],
+                         ids=["aniso", "iso", "aniso-default-rule", "iso-default-rule"])
+def test_c5_denoiser_branch_gradients(dev, iso, rule):
     """BASELINE c5's caller: the get_denoiser branch of src/nets/net_build.jl:113-128 -- Parallel(chcat) of
     5 x ADMMDeconvF2((), 50, rho, relu1, iso=use_iso) -- on a small RGB batch (2 x 3 planes of 256^2),
     branches in one grid; iso = true is the training default (src/configs/train_cfg.json:14),
     where the batch norm couples the 6 planes of a branch.  The gradient of a weighted sum of the output
     w.r.t. every branch's trainable lambda (deconv_admm.jl:107) against fp64 autograd of the oracle: for
-    branch i, lambda_bar = <xbar_i, d x_i / d lambda> with xbar_i = w_i * relu1'(x_i).  iso-default-rule: the
+    branch i, lambda_bar = <xbar_i, d x_i / d lambda> with xbar_i = w_i * relu1'(x_i).  *-default-rule: the
     library's plane-count rule at its default, under which these 30 planes run the 2-pass kernels over all five
     branches in one grid (the reference's training configuration, train_cfg.json:10-14)."""
     import oracle_torch
-    rule = iso == "rule"
-    iso = bool(iso)
     rng = np.random.default_rng(12)
     rhos = (0.002, 0.02, 0.2, 2.0, 4.0)
     br = [layers.ADMMDeconvF2((), 50, r, layers.relu1, iso=iso, rng=rng, device=dev) for r in rhos]

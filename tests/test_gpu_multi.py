@@ -48,14 +48,26 @@ def test_multi_forward_vs_oracle(dev):
         assert_parity(x[:, 3 * i:3 * i + 3], ref, what=f"branch {i}")
 
 
+@pytest.mark.parametrize("rule", [False, pytest.param(True, marks=pytest.mark.min_planes_rule)],
+                         ids=["per-plane", "default-rule"])
 @pytest.mark.parametrize("need_rho", [True, False], ids=["full-trajectory", "mask-bits"])
-def test_multi_backward_is_the_branches(dev, need_rho):
+def test_multi_backward_is_the_branches(dev, need_rho, rule):
+    """default-rule: 30 planes are below the fused kernels' plane count, so the merged grid runs the 2-pass
+    kernels over every branch's planes and each branch alone the same kernels: everything bitwise (the partial
+    rows are laid out per branch as a single solve's)."""
     n, B, P, K = 5, 2, 3, 10
     y = torch.from_numpy(synth.make_batch(B, 256, 256, None, P=P, sigma=0.1, g0=6)).to(dev)
     lams, rhos = _branch_scalars(dev, n, seed=5)
     xb = torch.randn((B, n * P, 256, 256), device=dev)
-    x, rec = admm_deconv.tvd_fft_multi(y, lams, rhos, K, record=True, need_rho=need_rho)
-    yb, lb, rb = admm_deconv.tvd_fft_multi_backward_recorded(rec, x, xb, need_rho=need_rho)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    try:
+        x, rec = admm_deconv.tvd_fft_multi(y, lams, rhos, K, record=True, need_rho=need_rho)
+        yb, lb, rb = admm_deconv.tvd_fft_multi_backward_recorded(rec, x, xb, need_rho=need_rho)
+        columns = _lib.profile_get(_lib.K_COLUMN)[1]
+    finally:
+        _lib.profile_enable(False)
+    assert columns == (2 * K if rule else 0), columns
     yb_sum = torch.zeros_like(y)
     for i in range(n):
         xi, reci = admm_deconv.tvd_fft_record(y, lams[i], rhos[i], None, False, K, need_rho=need_rho)
