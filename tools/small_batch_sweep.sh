@@ -8,8 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 O=gpurun_out/${TAG}_sweep.jsonl
 for iso in "--iso" ""; do
-    for lt in 0 4 2; do
-        for ct in 0 512 1024; do
+    for lt in ${LTS:-0 4 2}; do
+        for ct in ${CTS:-0 512 1024}; do
             echo "== $iso LINE_T=$lt COL_THREADS=$ct"
             timeout -k 10 120 python bench.py --config c5 $iso --batch 2 --steps 20 --warmup 3 \
                 --opt LINE_T=$lt --opt COL_THREADS=$ct > gpurun_out/${TAG}_one.json 2>> gpurun_out/${TAG}_sweep.err || exit $?
