@@ -129,26 +129,30 @@ static float time_one(const float4* a, const float4* h, float4* c, unsigned tile
 static const char* kName[] = {"read", "write", "copy", "solve"};
 
 template <int MODE, int U, bool BUF, int IL = 0, int AUXL = 0, int AUXS = 0>
-static void run(FILE* out, const float4* a, const float4* h, float4* c, size_t ws_bytes, int wpc, float* sink) {
+static void run(FILE* out, const float4* a, const float4* h, float4* c, size_t ws_bytes, int wpc, float* sink,
+                bool inplace = false) {
     // primary array size: read/write touch one array of ws; copy two of ws/2; solve s (ws*0.4) + s' (ws*0.4) +
     // h (ws*0.2): ws = 2|s| + |h| = 2.5|s|
     size_t prim = MODE == COPY ? ws_bytes / 2 : MODE == SOLVE ? ws_bytes * 2 / 5 : ws_bytes;
     const int grid = 256 * wpc / 4;                           // 256-thread workgroups = 4 waves each
     const size_t ts = (size_t)256 * U * (MODE == SOLVE ? 2 : 1);
     const unsigned tiles = (unsigned)(prim / 16 / ts / grid * grid);
+    if (tiles == 0) return;   // working set smaller than one tile per workgroup
     const size_t n4 = tiles * ts;
     double bytes = MODE == READ || MODE == WRITE ? n4 * 16.0 : MODE == COPY ? n4 * 32.0 : n4 * 16.0 * 2.5;
     int reps = (int)(20e9 / bytes) + 2;
-    float ms = time_one<MODE, U, BUF, IL, AUXL, AUXS>(a, h, c, tiles, grid, sink, reps);
+    float ms = time_one<MODE, U, BUF, IL, AUXL, AUXS>(a, h, inplace ? const_cast<float4*>(a) : c, tiles, grid, sink,
+                                                     reps);
     double tbs = bytes / (ms * 1e-3) / 1e12;
     const char* acc = BUF ? "buffer_dwordx4" : "global_dwordx4";
     const char* lay = IL ? "interleaved" : "chunked";
     fprintf(out, "{\"kernel\": \"%s\", \"access\": \"%s\", \"layout\": \"%s\", \"aux_load\": %d, \"aux_store\": %d, "
-                 "\"U\": %d, \"waves_per_cu\": %d, \"bytes\": %.0f, \"ms\": %.4f, \"TBps\": %.3f}\n",
-            kName[MODE], acc, lay, AUXL, AUXS, U, wpc, bytes, ms, tbs);
+                 "\"U\": %d, \"waves_per_cu\": %d, \"ws_bytes\": %zu, \"in_place\": %d, \"bytes\": %.0f, \"ms\": %.4f, "
+                 "\"TBps\": %.3f}\n",
+            kName[MODE], acc, lay, AUXL, AUXS, U, wpc, ws_bytes, (int)inplace, bytes, ms, tbs);
     fflush(out);
-    printf("%-5s %-14s %-11s aux %d/%-2d U=%d wpc=%2d %6.2f GB  %8.3f ms  %6.3f TB/s\n", kName[MODE], acc, lay, AUXL,
-           AUXS, U, wpc, bytes / 1e9, ms, tbs);
+    printf("%-5s %-14s %-11s aux %d/%-2d U=%d wpc=%2d ws %6.0f MB%s %6.2f GB  %8.3f ms  %6.3f TB/s\n", kName[MODE], acc,
+           lay, AUXL, AUXS, U, wpc, ws_bytes / 1048576.0, inplace ? " in place" : "", bytes / 1e9, ms, tbs);
     fflush(stdout);
 }
 
@@ -174,6 +178,7 @@ static void forms(FILE* out, const float4* a, const float4* h, float4* c, float*
 int main(int argc, char** argv) {
     FILE* out = argc > 1 ? fopen(argv[1], "w") : stdout;
     if (!out) { perror("open"); return 1; }
+    const bool cache_only = argc > 2 && argv[2][0] == 'c';   // section 4 only
     const size_t maxws = 8ull << 30;
     char *a, *c, *h;
     CK(hipMalloc(&a, maxws));
@@ -185,6 +190,19 @@ int main(int argc, char** argv) {
     const float4* A = (const float4*)a;
     const float4* H = (const float4*)h;
     float4* C = (float4*)c;
+    // 4) working sets around the 256 MiB Infinity Cache (the fused 256^2 solve holds 256 planes x 768 KiB = 192 MiB of
+    //    s and H^T y per wave of workgroups, rewritten in place every iteration): the solve mix, to a second array
+    //    and in place
+    for (size_t mb : {64, 128, 192, 256, 384, 768}) {
+        run<SOLVE, 4, true, 1>(out, A, H, C, mb << 20, 8, sink);
+        run<SOLVE, 4, true, 1>(out, A, H, C, mb << 20, 8, sink, true);
+        run<SOLVE, 2, true, 0>(out, A, H, C, mb << 20, 8, sink, true);
+        run<COPY, 4, true, 0>(out, A, H, C, mb << 20, 8, sink);
+    }
+    if (cache_only) {
+        if (out != stdout) fclose(out);
+        return 0;
+    }
     // 1) occupancy / unroll sweep at 4 GB
     for (int wpc : {8, 16, 32}) {
         both<READ, 4>(out, A, H, C, 4ull << 30, wpc, sink);
