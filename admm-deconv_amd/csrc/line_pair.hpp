@@ -24,6 +24,17 @@ namespace admm {
 
 #include "tw256.inc"
 
+// Instruction-count trims (round 5 experiment switches, off): 1 = the lane-pair add / subtract as one FMA with the
+// lane's sign, 2 = lane exchanges pinned on the caller's variable (no v_mov copy), 4 = no select for iteration 1's
+// zero s (plane_kernel.hip row_update, plane_iso.hip row_iso_a).  All three cut the c2 iteration loop from 12.4k
+// to 11.6k VALU per wave (tools/isa_mix.py), yet each alone made c2 5 % SLOWER (164k -> 156-161k img/s, A/B on
+// one box, profiles/r05_plane_xv_ab.jsonl): the removed instructions were independent filler between dependent
+// ones at 2 waves per SIMD, and issue stalls rose (SQ_WAIT_INST_ANY 0.296 -> 0.334 of wave cycles,
+// profiles/r05_plane_xv_sq.json).  All three together: c5 +2 %.  The kernel is bound by dependency latency.
+#ifndef PLANE_XV
+#define PLANE_XV 0
+#endif
+
 // v * W256^E (forward, W256 = exp(-2 pi i/256)) or v * conj(W256^E) (inverse)
 template <int E, bool INV>
 __device__ __forceinline__ float2 w256(float2 v) {
@@ -61,6 +72,18 @@ __device__ __forceinline__ float2 swap_pair(float2 v) {
                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, true)));
 }
 #endif
+// swap_pair of a value the caller uses again: the pin acts on the caller's variable itself, so the swap and the
+// later uses read the same (pinned) registers -- pinning a by-value copy made the compiler keep the original
+// alive beside it (two v_mov per register of every lane-pair combine)
+__device__ __forceinline__ float2 swap_pair_keep(float2& v) {
+#if defined(ADMM_SWAP_BPERMUTE) || !(PLANE_XV & 2)
+    return swap_pair(v);
+#else
+    __asm__ volatile("" : "+v"(v.x), "+v"(v.y));
+    return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0xB1, 0xF, 0xF, true)),
+                       __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, true)));
+#endif
+}
 
 // ---- in-register N-point FFT (N = 32 or 64), natural order in and out: N = 4 (n1) x N/4 (n2) -----
 //   X[k1 + 4 k2] = sum_{n2} W_{N/4}^{n2 k2} W_N^{n2 k1} sum_{n1} x[(N/4) n1 + n2] W4^{n1 k1}
@@ -136,32 +159,45 @@ __device__ __forceinline__ void fft64_reg_stage(float2 (&x)[64], float2* stg, fl
     }
 }
 
+// Lane A adds, lane B subtracts its own value from the partner's: one FMA with the lane's sign sg = +1 (A) / -1
+// (B), fma(mine, sg, oth) = mine + oth / oth - mine exactly (a single rounding either way, as the add / sub),
+// instead of both results and a select per component.
+__device__ __forceinline__ float lane_sign(bool hb) { return hb ? -1.0f : 1.0f; }
+__device__ __forceinline__ float2 pm_pair(float2 mine, float2 oth, float sg) {
+#if PLANE_XV & 1
+    return make_float2(fmaf(mine.x, sg, oth.x), fmaf(mine.y, sg, oth.y));
+#else
+    return sg < 0.0f ? csub(oth, mine) : cadd(mine, oth);
+#endif
+}
+
 // forward DIT combine across the pair: A: Z[k] = E[k] + W128^k O[k], B: Z[k+64] = E[k] - W128^k O[k]
 template <int K>
-__device__ __forceinline__ void combine_fwd(float2 (&x)[64], bool hb) {
+__device__ __forceinline__ void combine_fwd(float2 (&x)[64], bool hb, float sg) {
     if constexpr (K < 64) {
         float2 xk = x[K];
         // K = 32: W256^64 = -i is a swap of the fields, and `hb ? (y, -x) : (x, y)` on a register still in
         // the front end's S array becomes a select of field ADDRESSES -- S[32] then stays in scratch (the PSF
         // kernel: every access to it a scratch load / store).  The pin makes it a select of values.
         if constexpr (2 * K == 64) __asm__ volatile("" : "+v"(xk.x), "+v"(xk.y));
-        const float2 mine = hb ? w256<2 * K, false>(xk) : xk;
-        const float2 oth = swap_pair(mine);
-        x[K] = hb ? csub(oth, mine) : cadd(mine, oth);
+        float2 mine = hb ? w256<2 * K, false>(xk) : xk;
+        const float2 oth = swap_pair_keep(mine);
+        x[K] = pm_pair(mine, oth, sg);
         if constexpr ((K & 15) == 15) sched_fence();
-        combine_fwd<K + 1>(x, hb);
+        combine_fwd<K + 1>(x, hb, sg);
     }
 }
 
 // inverse split across the pair: A: E'[k] = Z[k] + Z[k+64], B: O'[k] = (Z[k] - Z[k+64]) W128^-k
 template <int K>
-__device__ __forceinline__ void split_inv(float2 (&x)[64], bool hb) {
+__device__ __forceinline__ void split_inv(float2 (&x)[64], bool hb, float sg) {
     if constexpr (K < 64) {
-        const float2 mine = x[K];
-        const float2 oth = swap_pair(mine);
-        x[K] = hb ? w256<2 * K, true>(csub(oth, mine)) : cadd(mine, oth);
+        float2 mine = x[K];
+        const float2 oth = swap_pair_keep(mine);
+        const float2 d = pm_pair(mine, oth, sg);
+        x[K] = hb ? w256<2 * K, true>(d) : d;
         if constexpr ((K & 15) == 15) sched_fence();
-        split_inv<K + 1>(x, hb);
+        split_inv<K + 1>(x, hb, sg);
     }
 }
 
@@ -191,7 +227,7 @@ template <int M>
 __device__ __forceinline__ void post_fwd_pairs(float2 (&x)[64], bool hb) {
     if constexpr (M < 32) {
         constexpr int Q = 64 - M;
-        const float2 pq = swap_pair(x[Q]), pm = swap_pair(x[M]);
+        const float2 pq = swap_pair_keep(x[Q]), pm = swap_pair_keep(x[M]);
         x[M] = post_fwd<M>(x[M], pq, hb);
         x[Q] = post_fwd<Q>(x[Q], pm, hb);
         if constexpr ((M & 7) == 7) sched_fence();
@@ -213,33 +249,34 @@ __device__ __forceinline__ void pre_inv_pairs(float2 (&x)[64], bool hb) {
 
 // one register of the inverse split (see split_inv)
 template <int K>
-__device__ __forceinline__ void split_one(float2 (&x)[64], bool hb) {
-    const float2 mine = x[K];
-    const float2 oth = swap_pair(mine);
-    x[K] = hb ? w256<2 * K, true>(csub(oth, mine)) : cadd(mine, oth);
+__device__ __forceinline__ void split_one(float2 (&x)[64], bool hb, float sg) {
+    float2 mine = x[K];
+    const float2 oth = swap_pair_keep(mine);
+    const float2 d = pm_pair(mine, oth, sg);
+    x[K] = hb ? w256<2 * K, true>(d) : d;
 }
 
 // pre-processing of pair (M, 64-M) fused with the split of both registers: each register is final for
 // the 64-point IFFT as soon as its pair is done, which keeps the live set small (pre then split as two
 // sweeps needed ~256 VGPRs and spilled; fused it fits with the FFT's own peak)
 template <int M>
-__device__ __forceinline__ void pre_split_pairs(float2 (&x)[64], bool hb) {
+__device__ __forceinline__ void pre_split_pairs(float2 (&x)[64], bool hb, float sg) {
     if constexpr (M < 32) {
         constexpr int Q = 64 - M;
-        const float2 pq = swap_pair(x[Q]), pm = swap_pair(x[M]);
+        const float2 pq = swap_pair_keep(x[Q]), pm = swap_pair_keep(x[M]);
         x[M] = pre_inv<M>(x[M], pq, hb);
         x[Q] = pre_inv<Q>(x[Q], pm, hb);
-        split_one<M>(x, hb);
-        split_one<Q>(x, hb);
+        split_one<M>(x, hb, sg);
+        split_one<Q>(x, hb, sg);
         if constexpr ((M & 3) == 3) sched_fence();
-        pre_split_pairs<M + 1>(x, hb);
+        pre_split_pairs<M + 1>(x, hb, sg);
     }
 }
 
 // z (spatial) -> packed half spectrum, in place
 __device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
     fft64_reg<false>(S);
-    combine_fwd<0>(S, hb);
+    combine_fwd<0>(S, hb, lane_sign(hb));
     sched_fence();
     // k = 0 (A): packed (X[0], X[128]) = (Re Z0 + Im Z0, Re Z0 - Im Z0); k = 64 (B): X[64] = conj Z[64]
     const float2 z0 = S[0];
@@ -251,26 +288,28 @@ __device__ __forceinline__ void line_forward_pair(float2 (&S)[64], bool hb) {
 
 // line_inverse_pair with z registers 32..63 delivered to the LDS staging slots (fft64_reg_stage)
 __device__ __forceinline__ void line_inverse_pair_staged(float2 (&S)[64], bool hb, float2* stg, float2* stg2) {
+    const float sg = lane_sign(hb);
     const float2 x0 = S[0];
     S[0] = hb ? make_float2(2.f * x0.x, -2.f * x0.y) : make_float2(x0.x + x0.y, x0.x - x0.y);
-    split_one<0>(S, hb);
+    split_one<0>(S, hb, sg);
     const float2 p32 = swap_pair(S[32]);
     S[32] = pre_inv<32>(S[32], p32, hb);
-    split_one<32>(S, hb);
-    pre_split_pairs<1>(S, hb);
+    split_one<32>(S, hb, sg);
+    pre_split_pairs<1>(S, hb, sg);
     sched_fence();
     fft64_reg_stage<true>(S, stg, stg2);
 }
 
 // packed half spectrum -> z (spatial), in place (unnormalised: 256 x)
 __device__ __forceinline__ void line_inverse_pair(float2 (&S)[64], bool hb) {
+    const float sg = lane_sign(hb);
     const float2 x0 = S[0];
     S[0] = hb ? make_float2(2.f * x0.x, -2.f * x0.y) : make_float2(x0.x + x0.y, x0.x - x0.y);
-    split_one<0>(S, hb);
+    split_one<0>(S, hb, sg);
     const float2 p32 = swap_pair(S[32]);
     S[32] = pre_inv<32>(S[32], p32, hb);
-    split_one<32>(S, hb);
-    pre_split_pairs<1>(S, hb);
+    split_one<32>(S, hb, sg);
+    pre_split_pairs<1>(S, hb, sg);
     sched_fence();
     fft64_reg<true>(S);
 }

@@ -44,6 +44,7 @@ __device__ __forceinline__ float bt_f(float tau, float r) {
 // q = (s1^2 + s2^2 of the lane's two pixels) to qst.  Neighbours as in row_update.
 __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t sst, rsrc_t fld, rsrc_t qst, float2* xb,
                                           float2* colbuf, int t, bool hb, bool first) {
+    (void)first;
     constexpr int PD = ISO_PD, NR = PD + 1;
     const int lane = t & 63, w = t >> 6;
     const bool top = lane < 2, bot = lane >= 62;
@@ -83,7 +84,7 @@ __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t ss
             for (int m = 0; m < 16; ++m) S[48 + m] = stg2[m * kPT];
             sched_fence();
         }
-        const float2 x = S[n];
+        float2 x = S[n];
         const float xl = swapf(hb ? (n == 0 ? x63y : S[(n + 63) & 63].y) : x.y);   // pixel before the lane's first
         const float2 xub = xbp[n];
         float2 xu = make_float2(lane_up2(x.x), lane_up2(x.y));   // line r-1
@@ -92,8 +93,11 @@ __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t ss
         const float4 a = sr[n % NR];
         const float2 f = fr[n % NR];
         // u_k = s_k - f s_k (z = f s, ops.jl:10), channel pairs (x, z) at pixel p and (y, w) at p + 1
+        // (first: sld and fld are resources of size 0, so a = f = 0 and u = 0 without a select)
         float4 u = make_float4(a.x - f.x * a.x, a.y - f.y * a.y, a.z - f.x * a.z, a.w - f.y * a.w);
+#if !(PLANE_XV & 4)
         if (first) u = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
         const float4 s = make_float4((x.x - xu.x) + u.x, (x.y - xu.y) + u.y, (x.x - xl) + u.z, (x.y - x.x) + u.w);
         bst4(sst, t * 16, n * kPT * 16, s);
         bst2(qst, t * 8, n * kPT * 8, make_float2(s.x * s.x + s.z * s.z, s.y * s.y + s.w * s.w));
@@ -357,7 +361,7 @@ __device__ __forceinline__ void row_isoadj_a(float2 (&S)[64], rsrc_t vst, rsrc_t
             for (int m = 0; m < 16; ++m) S[48 + m] = stg2[m * kPT];
             sched_fence();
         }
-        const float2 v = S[n];
+        float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
         const float2 vub = xbp[n];
         float2 vu = make_float2(lane_up2(v.x), lane_up2(v.y));
@@ -442,7 +446,7 @@ __device__ __forceinline__ void row_isoadj_b(float2 (&S)[64], rsrc_t s1p, rsrc_t
             S[63] = stg2[15 * kPT];
             sched_fence();
         }
-        const float2 v = S[n];
+        float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
         const float2 vub = xbp[n];
         float2 vu = make_float2(lane_up2(v.x), lane_up2(v.y));

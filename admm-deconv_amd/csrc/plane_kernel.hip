@@ -337,7 +337,14 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
 #ifndef PLANE_LANESHIFT
 #define PLANE_LANESHIFT 1
 #endif
-__device__ __forceinline__ float lane_up2(float v) {   // lane i <- lane i - 2
+// v is pinned in place (the caller's own variable, which it reads again): pinning a by-value copy kept the
+// original alive beside it, one v_mov per shift
+__device__ __forceinline__ float lane_up2(float& vr) {   // lane i <- lane i - 2
+#if PLANE_XV & 2
+    float& v = vr;
+#else
+    float v = vr;
+#endif
 #if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true);
@@ -346,7 +353,12 @@ __device__ __forceinline__ float lane_up2(float v) {   // lane i <- lane i - 2
     return __shfl_up(v, 2);
 #endif
 }
-__device__ __forceinline__ float lane_down2(float v) {   // lane i <- lane i + 2
+__device__ __forceinline__ float lane_down2(float& vr) {   // lane i <- lane i + 2
+#if PLANE_XV & 2
+    float& v = vr;
+#else
+    float v = vr;
+#endif
 #if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true);
@@ -370,8 +382,8 @@ __device__ __forceinline__ float2 finalize(float4 wn, float4 wnext, float2 hy, b
 // x (spatial, registers) -> s_k = Dx + clip(s_{k-1}) stored, S <- v = H^T y + rho D^T phi(s_k).
 // Branch-free inside: the boundary-line LDS traffic is done by every lane (reads broadcast from two
 // addresses, writes of non-boundary lanes go to a per-thread sink) so the chunk loop stays one block.
-// first: iteration 1, s_{k-1} = 0 (ops.jl:48-49 zero init) -- applied as a select on the clipped
-// value (the workspace holds garbage then), so one copy of this code serves every iteration.
+// first: iteration 1, s_{k-1} = 0 (ops.jl:48-49 zero init): the caller passes a resource of size 0 for sp then,
+// whose loads return 0 (clip(0) = 0), so one copy of this code serves every iteration without a select.
 //
 // Register budget: S (128 VGPRs) is the bulk.  The column buffer is idle here, so x of registers
 // 32..63 is parked in it (per-lane slots stg[m * 512 + t]) while registers 0..31 are processed; at
@@ -383,6 +395,7 @@ template <bool STAGED = false, bool MASK = false>
 __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sps, rsrc_t hp, float2* xb,
                                            float2* wb, float2* sink, float2* colbuf, int t, bool hb, bool first,
                                            float tau, float rho, rsrc_t mrs) {
+    (void)first;
 #ifndef PLANE_CH
 #define PLANE_CH 2
 #endif
@@ -486,14 +499,17 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
         for (int j = 0; j < CH; ++j) {
             const int n = n0 + j;
             const float4 so = sor[g % (PD + 1)][j];
-            const float2 x = S[n];
+            float2 x = S[n];
             const float xl = swapf(hb ? (n == 0 ? x63y : S[(n + 63) & 63].y) : x.y);   // pixel before this lane's first
             const float2 xub = xbp[n];
             float2 xu = make_float2(lane_up2(x.x), lane_up2(x.y));   // line r-1
             xu.x = top ? xub.x : xu.x;
             xu.y = top ? xub.y : xu.y;
+            // iteration 1 (first): so comes from a resource of size 0 (the caller's), i.e. 0, and clip(0) = 0: no select
             float4 uo = make_float4(clip_tau(so.x, tau), clip_tau(so.y, tau), clip_tau(so.z, tau), clip_tau(so.w, tau));
+#if !(PLANE_XV & 4)
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
 #ifndef PLANE_EXPT_NOSTORE
             bst4<PLANE_AUX_ST>(sps, t * 16, n * kPT * 16, s);
@@ -827,7 +843,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         const float4 s2 = MASK ? make_float4(0.f, 0.f, 0.f, 0.f) : s2r[n % NR];
         const float4 sb = sbr[n % NR];
         const float2 vo = vr[n % NR];
-        const float2 v = S[n];
+        float2 v = S[n];
         const float vl = swapf(hb ? (n == 0 ? v63y : S[(n + 63) & 63].y) : v.y);
         const float2 vub = xbp[n];
         float2 vu = make_float2(lane_up2(v.x), lane_up2(v.y));
