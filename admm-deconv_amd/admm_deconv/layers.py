@@ -219,11 +219,12 @@ class Parallel:
     When every branch is an ADMM layer the one-grid solve covers (the denoiser: ADMMDeconvF2((), K, ρ_i, σ),
     256 x 256, same K and prox; isotropic when no ρ needs a gradient and the branches' planes fit one wave of
     workgroups, ISO_MERGE_MAX_PLANES, or with merge="always"), all branches run as ONE solve (ops.tvd_fft_multi: every branch's
-    planes in one grid of the fused kernel, the output already in the chcat layout) and one reverse sweep;
-    each branch's bias and σ then apply to its slice.  The forward output, λ̄ and ρ̄ are bitwise those of the
-    branches run one by one through the same per-plane kernels (tests/test_gpu_multi.py, ADMM_OPT_MIN_PLANES = 0);
-    under the library's default plane-count rule a small branch alone runs the 2-pass kernels while the merged
-    grid runs the fused ones, so the two then agree to fp32 rounding, not bitwise (tests/test_gpu_default_rule.py).
+    planes in one grid -- of the fused kernels, or below the library's plane-count rule (96 / 112 planes in all) of
+    the 2-pass kernels -- the output already in the chcat layout) and one reverse sweep; each branch's bias and σ
+    then apply to its slice.  The forward output, λ̄ and ρ̄ are bitwise those of the branches run one by one
+    through the same kernels (tests/test_gpu_multi.py); when the merged grid is at or above the rule and a branch
+    alone below it (e.g. 5 branches x 24 planes), the two run different kernels and agree to fp32 rounding, not
+    bitwise (tests/test_gpu_default_rule.py).
     The input gradient matches to fp32 rounding in either case (branch_sum_kernel adds the branches' ȳ in a
     fixed order, not in autograd's per-branch accumulation order).  Otherwise the branches are independent, so on a ROCm device each runs on its own HIP stream
     (forward, and -- autograd replays a backward op on its forward's stream -- the adjoint too), then the
@@ -247,7 +248,8 @@ class Parallel:
         # isotropic: its one-grid solve is a launch per iteration either way.  Up to ISO_MERGE_MAX_PLANES planes in
         # all (about two waves of workgroups, one plane per CU), one grid per iteration halves the launches and
         # fills the chip better: the reference's training batch (train_cfg.json batch_size 2, 5 branches x 6
-        # planes) runs 229 img/s merged against 119 per-branch.  Above that, the branches on their own streams
+        # planes) runs 229 img/s merged against 119 per-branch (417 since round 5: below the plane-count rule the
+        # merged grid runs the 2-pass kernels).  Above that, the branches on their own streams
         # overlap one branch's batch-norm launches with the others' plane launches: batch 64 (960 planes) 1.11k
         # img/s per-branch against 1.03k merged.  merge="always" merges at any size.  The merged grid forms no
         # rho_bar.
