@@ -237,7 +237,8 @@ def bench_c5(args, dev):
         ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": f"{dom} (2-pass isotropic kernels, one grid of {nb} branches x {planes} planes)",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": None, "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(a["avg_ms"], 5)}
+                "traffic": load_traffic("c5iso2m", dom) if B == 2 else None, "algorithmic_bytes_per_launch": per[dom],
+                "avg_launch_ms": round(a["avg_ms"], 5)}
     elif merged and args.iso:
         # one grid of 5 x 192 planes per iteration / reverse step (plane_iso.hip, ADMM_MULTI_ISO)
         fwd, adj = iso_fused_bytes_per_px(K)
