@@ -200,6 +200,31 @@ def test_multi_branch_workspace_and_validation():
     assert _lib.backward_workspace_bytes(256, 256, 3, 2, 0, 0, True, 50, _lib.REC_MASKS) == fi
 
 
+@pytest.mark.parametrize("iso", [False, True], ids=["aniso", "iso"])
+def test_multi_branch_two_pass_layout(iso):
+    """Below the fused paths' plane counts (96 aniso / 112 iso in all) the multi-branch workspace is the 2-pass
+    kernels' (admm_capi.hip make_multi_layout two_pass: spectra, s state, natural-layout trajectory, per-branch
+    maps and partial rows), from the rule's threshold on the fused kernels' (lane-native tables); MIN_PLANES = 0
+    keeps the fused layout at every size.  c5 at batch 2 (5 x 6 planes) is below it."""
+    fl = (_lib.MULTI_ISO if iso else 0)
+    px, K, nb = 256 * 256, 50, 5
+    thr = 112 if iso else 96
+    for rec in (0, _lib.MULTI_RECORD):
+        small = _lib.multi_workspace_bytes(256, 256, 3, 2, nb, K, fl | rec)      # 30 planes: 2-pass
+        with _lib.option("MIN_PLANES", 0):
+            fused_small = _lib.multi_workspace_bytes(256, 256, 3, 2, nb, K, fl | rec)
+        assert small != fused_small
+        planes = 30
+        # two spectra of 4 B/px per plane at least, and (recording) the natural s trajectory of 8 B/px per slot
+        assert small >= 2 * planes * px * 4 + (49 * planes * px * 8 if rec else 0)
+        # the threshold, in planes in all (P * B * nbranch): one plane per image, nbranch = thr below / at it
+        below = _lib.multi_workspace_bytes(256, 256, 1, 1, thr - 1, K, fl | rec)
+        at = _lib.multi_workspace_bytes(256, 256, 1, 1, thr, K, fl | rec)
+        with _lib.option("MIN_PLANES", 0):
+            assert _lib.multi_workspace_bytes(256, 256, 1, 1, thr, K, fl | rec) == at
+            assert _lib.multi_workspace_bytes(256, 256, 1, 1, thr - 1, K, fl | rec) != below
+
+
 @pytest.mark.parametrize("case", __import__("paths_table").CASES, ids=[c[0] for c in __import__("paths_table").CASES])
 def test_path_decision_table(case):
     """Every (shape, prox, PSF, call, record flags, options) combination takes its intended path: the library's
