@@ -110,9 +110,12 @@ def parse():
                     help="c5 --iso: the branches in one grid (ADMM_MULTI_ISO) at any batch (default: only when all their planes fit one wave of workgroups, layers.ISO_MERGE_MAX_PLANES)")
     ap.add_argument("--iso", action="store_true",
                     help="c5 only: isotropic (BT) prox in the layers (use_iso, src/configs/train_cfg.json:14)")
-    ap.add_argument("--graph", action="store_true",
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
                     help="c5: capture the whole training step (forward, loss, adjoint, update) in one HIP graph and "
-                         "replay it (small batches are launch-bound: the reference's train_cfg.json batch 2)")
+                         "replay it.  Default: on when the merged branches run the 2-pass kernels (below the "
+                         "library's plane-count rule: the reference's train_cfg.json batch 2), whose ~400 launches "
+                         "per step make the step launch-bound (profiles/r05_c5_small_batch_graph.jsonl); off above")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
     return ap.parse_args()
 
 
@@ -179,6 +182,13 @@ def bench_c5(args, dev):
 
     run = step
     graph = None
+    if args.graph is None:
+        # the merged grid below the plane-count rule (ADMM_OPT_MIN_PLANES default; 96 aniso / 112 iso planes in
+        # all) runs the 2-pass kernels: ~100 launches per direction and branch set, so one graph per step pays
+        # (c5 batch 2: iso 401 -> 418, aniso 578 -> 617 img/s on one box); above it the step is one launch per
+        # solve (aniso) or per iteration on per-branch streams (iso), where a graph gains nothing or loses
+        args.graph = bool(merged and _lib.get_option("MIN_PLANES") == -1 and
+                          len(branch) * B * P < (112 if args.iso else 96))
     if args.graph:
         # warm up on a side stream (allocations, recordings registry, kernel attributes), then capture one whole
         # step; replays re-run every kernel of it (the gradients are recomputed, not accumulated: grad is None
@@ -217,17 +227,19 @@ def bench_c5(args, dev):
             kernels[name] = {"launches_per_step": n, "avg_ms": ms / n, "total_ms_per_step": ms}
     roof = None
     planes = B * P
-    if merged and args.iso and "column" in kernels:
+    if merged and "column" in kernels:
         # below the plane-count rule (the reference's training batch of 2: 30 planes) the merged grid runs the
-        # 2-pass isotropic kernels over all branches' planes (admm_launch.hip run_multi_2pass_iso_*).  Algorithmic
-        # bytes per pixel of a launch, per class (the per-branch f / |s| / R maps are L2-resident, not counted):
+        # 2-pass kernels over all branches' planes (admm_launch.hip run_multi_2pass_*).  Algorithmic bytes per
+        # pixel of a launch, per class (the per-branch f / |s| / R maps are L2-resident, not counted):
         #   column  packed line spectrum in + out                                           8
-        #   line    iso_a: spectrum 4, s_k 8, s_k+1 8 | iso_b: s 8, H^T y 4, spectrum 4    (20 + 16) / 2
-        #   adjoint iso_adj_a: spectrum 4, s_k-1 8, sbar 8, vbar 4, Vsum 8 | iso_adj_b: vbar 4, sbar 8, s_k-1 8,
-        #           sbar out 8, spectrum 4                                                  (32 + 32) / 2
+        #   iso     line    iso_a: spectrum 4, s_k 8, s_k+1 8 | iso_b: s 8, H^T y 4, spectrum 4    (20 + 16) / 2
+        #           adjoint iso_adj_a: spectrum 4, s_k-1 8, sbar 8, vbar 4, Vsum 8 | iso_adj_b: vbar 4, sbar 8,
+        #                   s_k-1 8, sbar out 8, spectrum 4                                        (32 + 32) / 2
+        #   aniso   line    spectrum in 4 + out 4, s_k-1 8, s_k 8, H^T y 4                              28
+        #           adjoint line_adj: spectrum in 4 + out 4, s_k-1 8, sbar in 8 + out 8 (no rho_bar, no y_bar)  32
         nb = len(branch)
         px = nb * planes * M * N
-        per = {"column": 8 * px, "line": 18 * px, "adjoint": 32 * px}
+        per = {"column": 8 * px, "line": (18 if args.iso else 28) * px, "adjoint": 32 * px}
         for k, b in per.items():
             if k in kernels:
                 kernels[k]["algorithmic_bytes_per_launch"] = b
@@ -235,10 +247,11 @@ def bench_c5(args, dev):
         dom = max((k for k in per if k in kernels), key=lambda k: kernels[k]["total_ms_per_step"])
         a = kernels[dom]
         ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
-        roof = {"bound": "hbm", "kernel": f"{dom} (2-pass isotropic kernels, one grid of {nb} branches x {planes} planes)",
+        roof = {"bound": "hbm", "kernel": f"{dom} (2-pass {'isotropic ' if args.iso else ''}kernels, one grid of {nb} "
+                                          f"branches x {planes} planes)",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("c5iso2m", dom) if B == 2 else None, "algorithmic_bytes_per_launch": per[dom],
-                "avg_launch_ms": round(a["avg_ms"], 5)}
+                "traffic": load_traffic("c5iso2m", dom) if (B == 2 and args.iso) else None,
+                "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(a["avg_ms"], 5)}
     elif merged and args.iso:
         # one grid of 5 x 192 planes per iteration / reverse step (plane_iso.hip, ADMM_MULTI_ISO)
         fwd, adj = iso_fused_bytes_per_px(K)
