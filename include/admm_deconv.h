@@ -205,9 +205,12 @@ int admm_tvd_backward_recorded_dev_f32(const float* y, const float* x_bar, float
  * of y with its own λ_i, ρ_i (device pointers: lambda[i], rho[i] -- host arrays of `nbranch` device
  * pointers) and writes the chcat layout: x_out is Julia (M, N, nbranch*P, B) == C
  * `float[B][nbranch*P][N][M]`, branch i's channels at i*P .. i*P+P-1 -- the output of
- * `Parallel(chcat, ...)` itself, before the layers' bias / σ.  All nbranch*P*B planes run in one grid of
- * the fused kernel, so no CU idles between branches.  256 x 256, no PSF, at most 65,280
- * planes in total (nbranch*P*B); the same results, bitwise, as nbranch separate solves.
+ * `Parallel(chcat, ...)` itself, before the layers' bias / σ.  All nbranch*P*B planes run in one grid --
+ * of the fused kernels, or, below the plane-count rule (ADMM_OPT_MIN_PLANES at its default: fewer than 96
+ * planes in all anisotropic / 112 isotropic), of the 2-pass kernels, which spread every plane over many
+ * workgroups (the training batch of 2: 30 planes) -- so no CU idles between branches.  256 x 256, no PSF,
+ * at most 65,280 planes in total (nbranch*P*B); the same results, bitwise, as nbranch separate solves
+ * through the same kernels.  The workspace size follows the rule (admm_tvd_multi_workspace_bytes).
  * flags: ADMM_MULTI_RECORD (1) records the trajectory for admm_tvd_backward_multi_recorded_dev_f32
  *        (the workspace then holds it until the replay); | ADMM_REC_MASKS (2) as above (no rho_bar);
  *        | ADMM_MULTI_ISO (4): isotropic prox (use_iso) -- the split-iteration kernels of plane_iso.hip,
