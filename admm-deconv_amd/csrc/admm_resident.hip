@@ -46,7 +46,9 @@ constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 p
 #define RS_PD 3                           // rows of update loads in flight ahead of the row being computed (2-5 within 1-2 %, 3 best: profiles/r04v_resident_pd.txt)
 #endif
 #ifndef RS_RAD
-#define RS_RAD 16
+// radix cap 25: the 250- and 200-point transforms run as 2 passes ({10, 25}, {20, 10}) instead of 3; at 250^2 x 256
+// 92.6k -> 98.9k img/s, 200^2 129k -> 167k, the other compiled shapes keep their plans (profiles/r05_resident_rad25.log)
+#define RS_RAD 25
 #endif
 #ifndef RS_PDI
 #define RS_PDI 4                          // the same for the isotropic A / B phases (3: 250^2 iso 3.78 -> 3.93 ms)
