@@ -427,24 +427,47 @@ __device__ __forceinline__ Thr thr_of(float2* buf, const float2* twm, const floa
 }
 
 // ---- column phase, chunk C: bins [kc0, kc1) = registers [C NR, C NR + NR) ---------------------------------
+// Three parts: the chunk's registers into the column buffer (column_stage<C>), the transforms with x Ct between
+// them (column_passes, the chunk given at run time: LDS and Ct only, no spectrum register), and the read-back
+// (column_unstage<C>).  column_phase runs the chunks as a loop that is NOT unrolled, so the passes' code exists
+// once instead of once per chunk (RS_COLSHARE; at 250^2 the kernel's iteration loop otherwise exceeds the 64 KiB
+// instruction cache two CUs share, DESIGN.md s5 "Round 5, resident").
+#ifndef RS_COLSHARE
+#define RS_COLSHARE 1
+#endif
 template <int MM, int NN, int C, int NREG>
-__device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
+__device__ __forceinline__ void column_stage(const float2 (&S)[NREG], const Thr& th,
+                                             int kc = imin(Geo<MM, NN>::H, (C + 1) * Geo<MM, NN>::KBC) - C * Geo<MM, NN>::KBC) {
     using G = Geo<MM, NN>;
-    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
-    using RD = Rad<NN>;
-    constexpr int kc0 = C * G::KBC, kc1 = imin(G::H, kc0 + G::KBC), kc = kc1 - kc0;
-    constexpr int KB = G::KBC, FS = G::FS, H = G::H, P = RD::P, NR = G::NR, R0 = C * NR;
-    float2* buf = th.buf;
+    constexpr int FS = G::FS, NR = G::NR, R0 = C * NR;
     if (th.kk < kc) {   // stores only: the spectrum registers are not written here
-        float2* col = buf + th.kk * FS;
+        float2* col = th.buf + th.kk * FS;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int j = r * G::LS + th.jt;
             if (r < NR - 1 || j < NN) col[j] = S[R0 + r];
         }
     }
+}
+template <int MM, int NN, int C, int NREG>
+__device__ __forceinline__ void column_unstage(float2 (&S)[NREG], const Thr& th,
+                                               int kc = imin(Geo<MM, NN>::H, (C + 1) * Geo<MM, NN>::KBC) - C * Geo<MM, NN>::KBC) {
+    using G = Geo<MM, NN>;
+    constexpr int NR = G::NR, R0 = C * NR;
+    // every thread reads back every register of the chunk (threads past the chunk's bins: a valid column,
+    // values never used; padding lines j >= NN: the column's padding slots, never used either)
+    const float2* col = th.buf + imin(th.kk, kc - 1) * G::FS;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) S[R0 + r] = col[r * G::LS + th.jt];
+}
+// the staged chunk's bins [kc0, kc0 + kc): dim-2 FFT, x Ct at the slot's frequency, IFFT (barrier before and after)
+template <int MM, int NN>
+__device__ __forceinline__ void column_passes(int kc0, int kc, const Thr& th, const float* __restrict__ Ct) {
+    using G = Geo<MM, NN>;
+    using RD = Rad<NN>;
+    constexpr int KB = G::KBC, FS = G::FS, H = G::H, P = RD::P;
     __syncthreads();
-    const Acc<FS> a{buf};
+    const Acc<FS> a{th.buf};
     dif_passes<NN, 0, P - 1, false, false, FS>(KB, th.twn, a);
     // last DIF pass (S = 1: no twiddles) -> x Ct at the slot's frequency -> first DIT pass, in registers
     {
@@ -485,13 +508,45 @@ __device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, 
     }
     __syncthreads();
     dit_passes<NN, 0, P - 1, true, false, FS>(KB, th.twn, a);
-    {   // every thread reads back every register of the chunk (threads past the chunk's bins: a valid column,
-        // values never used; padding lines j >= NN: the column's padding slots, never used either)
-        const float2* col = buf + imin(th.kk, kc - 1) * FS;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) S[R0 + r] = col[r * G::LS + th.jt];
-    }
+}
+template <int MM, int NN, int C, int NREG>
+__device__ __forceinline__ void column_chunk(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
+    using G = Geo<MM, NN>;
+    const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
+    constexpr int kc0 = C * G::KBC, kc1 = imin(G::H, kc0 + G::KBC);
+    column_stage<MM, NN, C>(S, th);
+    column_passes<MM, NN>(kc0, kc1 - kc0, th, Ct);
+    column_unstage<MM, NN, C>(S, th);
     __syncthreads();
+}
+// all column chunks of an iteration
+template <int MM, int NN, int NREG>
+__device__ __forceinline__ void column_phase(float2 (&S)[NREG], const Thr& th0, const float* __restrict__ Ct) {
+    using G = Geo<MM, NN>;
+    if constexpr (RS_COLSHARE && G::NCC > 1) {
+        // chunk c is always register group 0: after each chunk the groups rotate by one (NCC rotations = identity),
+        // so every register is written unconditionally (no phi of an old and a new value per register)
+        constexpr int NR = G::NR;
+#pragma unroll 1
+        for (int c = 0; c < G::NCC; ++c) {
+            const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
+            const int kc0 = __builtin_amdgcn_readfirstlane(c) * G::KBC;
+            const int kc = imin(G::H, kc0 + G::KBC) - kc0;
+            column_stage<MM, NN, 0>(S, th, kc);
+            column_passes<MM, NN>(kc0, kc, th, Ct);
+            column_unstage<MM, NN, 0>(S, th, kc);
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float2 t0 = S[r];
+#pragma unroll
+                for (int g = 0; g + 1 < G::NCC; ++g) S[g * NR + r] = S[(g + 1) * NR + r];
+                S[(G::NCC - 1) * NR + r] = t0;
+            }
+        }
+    } else {
+        static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th0, Ct); });
+    }
 }
 
 // ---- line phase, chunk C: lines [jc0, jc1) ---------------------------------------------------------------
@@ -1043,7 +1098,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #pragma unroll 1
     for (int it = 1; it <= maxit; ++it) {
 #ifndef RS_SKIP_COL
-        static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+        column_phase<MM, NN>(S, th, Ct);
 #endif
         if (it == maxit) {
             static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
@@ -1128,7 +1183,7 @@ __global__ __launch_bounds__(kNT) void resident_iso_kernel(const float* __restri
     } else {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kIsoB>(S, hs, th, la); });
     }
-    static_for<0, G::NCC>([&](auto ic) { column_chunk<MM, NN, decltype(ic)::value>(S, th, Ct); });
+    column_phase<MM, NN>(S, th, Ct);
     if (k == K - 1) {
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
         return;
