@@ -59,6 +59,11 @@ constexpr int kNT = 512;                  // threads per workgroup (8 waves, 2 p
 #ifndef RS_U2MAX
 #define RS_U2MAX 10
 #endif
+#ifndef RS_INPLACE
+// the anisotropic update rewrites s in place instead of ping-ponging two buffers: 256 planes at 250^2 re-stream
+// 192 MiB per iteration instead of 320, inside the 256 MiB Infinity Cache (DESIGN.md s5 "Round 5, resident")
+#define RS_INPLACE 1
+#endif
 constexpr int kRad = RS_RAD;              // radix cap of every transform
 constexpr int kLdsBytes = 160 * 1024;     // gfx950 LDS per CU
 
@@ -565,6 +570,7 @@ struct LineArgs {
     bool first;
     const float* fm;      // isotropic: the batch's BT factor map f_k (M x N, L2-resident)
     float* q;             // isotropic: this plane's q = s1^2 + s2^2 of s_{k+1} (the batch norm's input)
+    float l0[4];          // update: s channel 0 of line 0 (wave 0's lanes), held from chunk 0 to the last chunk
 };
 
 __device__ __forceinline__ float2 lane_swap(float2 v) {   // value of lane t ^ 1 (DPP quad_perm [1, 0, 3, 2])
@@ -605,7 +611,7 @@ __device__ __forceinline__ float2 zsep(float2 z, float2 zm, bool odd) {
 // register of lines 0, 1 (the last chunk's halo B), saved before the update phase: by the time a chunk stages
 // them, the chunk that owns those lines has already replaced them with the next iteration's spectra.
 template <int MM, int NN, int C, int MODE, int NREG, int NH>
-__device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)[NH], const Thr& th0, const LineArgs& a) {
+__device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)[NH], const Thr& th0, LineArgs& a) {
     using G = Geo<MM, NN>;
     const Thr th = thr_of<MM, NN>(th0.buf, th0.twm, th0.twn);
     using RD = Rad<MM>;
@@ -787,6 +793,7 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         constexpr bool SC = G::kScr;
         const int scr = 2 * G::BUF + w * 2 * MM;
         PV vf[QG], vl[QG];
+        PV s0a[QG];   // RS_INPLACE: s channel 0 of the wave's first row, stored after the barrier
 #ifdef RS_SKIP_ROWS   // timing experiments only: no row update (wrong results)
         if (false) {
 #else
@@ -803,7 +810,13 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                     PV s0;
 #pragma unroll
                     for (int g = 0; g < GP; ++g) s0.v[g] = (xa.v[g] - xb.v[g]) + clipf(o.v[g], tau);
+#if RS_INPLACE
+                    // stored after the block barrier below: the previous wave still reads this row's old channel 0
+                    // (its last row's s0 of line j + 1), and in place that would be the new value
+                    s0a[q] = s0;
+#else
                     st(rsn, q, so, s0);
+#endif
 #pragma unroll
                     for (int g = 0; g < GP; ++g) w0c[q].v[g] = prox_w(s0.v[g], tau);
                 }
@@ -919,6 +932,42 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
                 if (ub > ua) put(q, row(ub), SC ? xget(scr + 1, q) : vl[q]);
             }
         }
+#if RS_INPLACE
+        // the first rows' channel 0 (every wave's row loop, which reads the next wave's first row, is done).  Line 0
+        // (chunk 0, wave 0) waits for the last chunk when there are several: that chunk's last wave reads line 0's
+        // old channel 0 as its line j + 1
+        {
+            static_assert(QG * GP <= 4, "LineArgs::l0 holds 4 floats");
+            const unsigned sof = 4u * (unsigned)((jc0 + ua - 2) * MM);
+            if constexpr (C == 0 && G::NLC > 1) {
+                if (w == 0) {
+#pragma unroll
+                    for (int q = 0; q < QG; ++q)
+#pragma unroll
+                        for (int g = 0; g < GP; ++g) a.l0[q * GP + g] = s0a[q].v[g];
+                } else if (ub >= ua) {
+#pragma unroll
+                    for (int q = 0; q < QG; ++q) st(rsn, q, sof, s0a[q]);
+                }
+            } else {
+                if (ub >= ua) {
+#pragma unroll
+                    for (int q = 0; q < QG; ++q) st(rsn, q, sof, s0a[q]);
+                }
+            }
+            if constexpr (C == G::NLC - 1 && G::NLC > 1) {
+                if (w == 0) {
+#pragma unroll
+                    for (int q = 0; q < QG; ++q) {
+                        PV l;
+#pragma unroll
+                        for (int g = 0; g < GP; ++g) l.v[g] = a.l0[q * GP + g];
+                        st(rsn, q, 0u, l);
+                    }
+                }
+            }
+        }
+#endif
         __syncthreads();
         // ---- forward DIT of the chunk's pairs (v at dpos order -> natural z) ----
         dit_passes<MM, 0, P, false, true, MM>(T / 2, th.twm, Acc<MM>{buf + MM});
@@ -1110,8 +1159,8 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
             sn = traj + (size_t)(it - 1) * traj_stride;
             so = it >= 2 ? traj + (size_t)(it - 2) * traj_stride : sn;
         } else {
-            sn = (it & 1) ? sA : sB;
-            so = (it & 1) ? sB : sA;
+            sn = (!RS_INPLACE && (it & 1)) ? sA : sB;
+            so = RS_INPLACE ? sn : (it & 1) ? sB : sA;
         }
         la.sn = sn + plane * 2 * MN;
         la.so = so + plane * 2 * MN;
