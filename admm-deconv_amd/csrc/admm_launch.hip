@@ -311,7 +311,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         rc = ln.run(ADMM_K_PLANE, [&] {
             return pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
                                    planes, s, tr.m ? nullptr : reinterpret_cast<float4*>(tr.s),
-                                   opt(ADMM_OPT_PLANE_STAGGER), nullptr, tr.m);
+                                   fwd_stagger(), nullptr, tr.m);
         });
         return rc;
     }
@@ -389,7 +389,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                                     twN, prm, maxit, tr, red);
         return ln.run(ADMM_K_PLANE, [&] {
             return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, np * 2 * MN, x_out, Ct, twM, twN, prm,
-                                    maxit, opt(ADMM_OPT_PLANE_STAGGER));
+                                    maxit, fwd_stagger());
         });
     }
     // experiment (round 5): the 512 x 512 anisotropic solve as one persistent team launch (team512_kernel)
@@ -559,7 +559,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     if (res) {
         return ln.run(ADMM_K_PLANE, [&] {
             return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit,
-                                    opt(ADMM_OPT_PLANE_STAGGER));
+                                    fwd_stagger());
         });
     }
     for (int it = 1; it <= maxit; ++it) {
@@ -797,7 +797,7 @@ int launch_backward(int phases, const float* y, const float* x_bar, float* y_bar
         rc = ln.run(ADMM_K_ADJ, [&] {
             return pk::launch_plane_adj(x_bar, ws + bl.f.F, tr.m ? static_cast<const void*>(tr.m) : tr.s, dxK,
                                        reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s,
-                                       nullptr, tr.m != nullptr, opt(ADMM_OPT_PLANE_STAGGER));
+                                       nullptr, tr.m != nullptr, adj_stagger());
         });
         if (rc) return rc;
         red_rows = (int)planes;
@@ -1337,7 +1337,7 @@ int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int 
         return admm::plane::launch_plane(y, x_out, ws + L.F, false, reinterpret_cast<float2*>(ws + L.hln),
                                          reinterpret_cast<float4*>(ws + L.sln), prm, maxit, planes, s,
                                          rec && !masks ? reinterpret_cast<float4*>(ws + L.traj) : nullptr,
-                                         opt(ADMM_OPT_PLANE_STAGGER), &br,
+                                         fwd_stagger(), &br,
                                          masks ? reinterpret_cast<unsigned*>(ws + L.traj) : nullptr);
     });
     if (rc) return rc;
@@ -1430,7 +1430,7 @@ int launch_backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, f
     rc = ln.run(ADMM_K_ADJ, [&] {
         return admm::plane::launch_plane_adj(x_bar, ws + L.F, ws + L.traj, dxK, reinterpret_cast<float4*>(ws + L.sbar),
                                              reinterpret_cast<float2*>(ws + L.vsl), vbuf, part,
-                                             prm, K, planes, s, &br, masks, opt(ADMM_OPT_PLANE_STAGGER));
+                                             prm, K, planes, s, &br, masks, adj_stagger());
     });
     if (rc) return rc;
     double* rt = reinterpret_cast<double*>(ws + L.rt);

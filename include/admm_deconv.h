@@ -240,7 +240,9 @@ enum {
     ADMM_OPT_COL_THREADS = 3,    /* 0 (default): policy; 256, 512 or 1024 threads per column block       */
     ADMM_OPT_GEN_TM = 4,         /* 0 (default 2048): runtime-length line block points, 256..8192        */
     ADMM_OPT_GEN_KN = 5,         /* 0 (default 1024): runtime-length column block points, 256..8192      */
-    ADMM_OPT_PLANE_STAGGER = 6,  /* 0 (default): fused kernel odd-workgroup start delay, 10 ns ticks     */
+    ADMM_OPT_PLANE_STAGGER = 6,  /* fused kernels' odd-workgroup start delay, 10 ns ticks: 0 (default):
+                                    none in the forward kernels, 3500 in the 256^2 reverse sweep; > 0: that
+                                    delay in both; -1: none anywhere                                       */
     ADMM_OPT_SMOOTH = 7,         /* 1 (default): compile-time-plan kernels for the listed non-power-of-two
                                     lengths (admm_smooth.hip); 0: runtime plans for every such shape;
                                     2 / 3: compiled, column plans forced increasing / decreasing (sweeps)  */
