@@ -950,9 +950,14 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
                                                            Branches br, int stagger_ticks) {
     // Phase stagger (experiment option ADMM_OPT_PLANE_STAGGER): odd workgroups of the first wave start
     // `stagger_ticks` of the 100 MHz realtime clock late, so that two CU groups' row phases alternate.
-    if (stagger_ticks > 0 && (blockIdx.x & 1) && blockIdx.x < 256) {
+#ifndef ADJ_STAGGER_GROUPS
+#define ADJ_STAGGER_GROUPS 2   // phase groups of the first wave: group g = blockIdx mod G starts g / (G - 1) x stagger late
+#endif
+    constexpr unsigned kSG = ADJ_STAGGER_GROUPS;
+    if (stagger_ticks > 0 && (blockIdx.x % kSG) && blockIdx.x < 256) {
+        const unsigned long long d = (unsigned long long)stagger_ticks * (blockIdx.x % kSG) / (kSG - 1);
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger_ticks) __builtin_amdgcn_s_sleep(10);
+        while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(10);
     }
     const BranchOf bo = branch_of(br, blockIdx.x);
     Cf += (size_t)bo.i * br.tab_f;
