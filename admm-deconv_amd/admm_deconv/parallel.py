@@ -158,17 +158,28 @@ class ShardGather:
         if int(flag.item()) == 1:
             return True
         self.close()
+        self.closed = False   # only the peer mappings are gone: the RCCL path takes over
         self.recv, self.remote = None, None
         return False
 
     def close(self):
-        """Unmap the peer receive buffers this rank opened (engine "ipc"); the object is unusable afterwards."""
-        for base in getattr(self, "_mapped", []):
+        """Unmap the peer receive buffers this rank opened (engine "ipc"); the object is unusable afterwards.
+        The copies into the peer's mapping run asynchronously on the comm stream (stream_only steps never wait
+        for them), so the stream is drained before the mapping goes away; later steps raise."""
+        mapped = getattr(self, "_mapped", [])
+        if mapped and getattr(self, "comm", None) is not None:
+            try:
+                self.comm.synchronize()
+            except Exception:   # noqa: BLE001 -- a failed device: unmapping below is all that is left
+                pass
+        for base in mapped:
             try:
                 _lib.ipc_close(base, self.y.device.index)
             except Exception:   # noqa: BLE001 -- best effort at teardown
                 pass
         self._mapped = []
+        self.remote = None
+        self.closed = True
 
     def __del__(self):
         if getattr(self, "_mapped", None):
@@ -205,6 +216,8 @@ class ShardGather:
                         self.comm.cuda_stream)
 
     def step(self):
+        if getattr(self, "closed", False):
+            raise RuntimeError("ShardGather: step() after close()")
         if (self.engine == "ipc" and self.world > 1 and not self.stream_only and self.i >= 1
                 and self.consumed != self.i - 1):
             raise RuntimeError("ShardGather(engine='ipc'): call gathered() (on every rank) after each step before the "

@@ -159,6 +159,8 @@ struct RecTag {
     int dev_scalars;
     int masks;   // the trajectory holds ST mask bytes (ADMM_REC_MASKS): no rho_bar
     int nbr;     // branches of a multi-branch recording (1: a single solve)
+    int sharded; // recorded with a batch reducer: sharded calls plan without the plane-count rule, so a replay
+                 // with (or without) one must match or it could plan another sweep than the trajectory's layout
     bool operator==(const RecTag& o) const { return std::memcmp(this, &o, sizeof(RecTag)) == 0; }
 };
 std::mutex g_rec_mu;
@@ -252,6 +254,7 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
     if (rc) return rc;
     RecTag tag = make_tag(M, N, P, B, kh, kw, iso, maxit, want_h, sc);
     tag.masks = use_masks;
+    tag.sharded = red != nullptr;
     if (phases == 2) {
         std::lock_guard<std::mutex> lk(g_rec_mu);
         auto it = g_rec.find(workspace);
@@ -260,7 +263,8 @@ int run_backward(int phases, int rec_flags, const float* y, const float* x_bar, 
                                         "on the same workspace overwrites it)");
         if (!(it->second == tag))
             return fail(ADMM_E_INVALID, "replay does not match its recording (shape, PSF, iso, maxit, h_bar request, "
-                                        "lambda / rho or library options changed between record and replay)");
+                                        "lambda / rho, library options or the batch reducer (sharded or not) changed "
+                                        "between record and replay)");
         if (use_masks && rho_bar)
             return fail(ADMM_E_INVALID, "recorded with ADMM_REC_MASKS (soft-threshold branches only / the fused isotropic "
                                         "trajectory): rho_bar cannot be formed from it; record without the flag to get rho_bar");

@@ -293,8 +293,8 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 //   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar), in fp64:
 //            K terms per bin, later scaled by C^2 in hbarA_kernel
 // ----------------------------------------------------------------------------------------------
-// The body takes the block's (slot block, plane) explicitly so that a persistent kernel can run it too
-// (team512_kernel below); column_kernel is the one-launch-per-pass form.
+// The body takes the block's (slot block, plane) explicitly (a persistent kernel can run it too: the round-5 team
+// launch, tools/variants/team512.patch); column_kernel is the one-launch-per-pass form.
 template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
 __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* dst, const float* __restrict__ Ct,
                                             const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
@@ -686,93 +686,6 @@ __global__ __launch_bounds__(NT) void line_kernel(const float2* __restrict__ spe
                                                   const float* __restrict__ hty, const float2* __restrict__ twM, int N,
                                                   const float* __restrict__ prm, int s_zero, Branches br = kOneSolve) {
     line_body<L, T, NT>(xcd_block(), spec1, spec0, s_old, s_new, hty, twM, N, prm, s_zero, br);
-}
-
-// ----------------------------------------------------------------------------------------------
-// TEAM512 (experiment, round 5; VERDICT r04 Next #4): the 2-pass solve at 512 x 512 as ONE persistent
-// launch.  Four 1024-thread workgroups (a "team", placed on one XCD by the dispatch order: workgroup b runs
-// on XCD b mod 8) solve one plane at a time, all K iterations: each member runs the column pass on a quarter
-// of the plane's spectral slots and the line pass on a quarter of its lines, with a team barrier in place of
-// every kernel boundary.  The spectrum still moves through global memory between the passes -- the
-// question this prototype answers is whether it then stays in the XCD's L2 / the Infinity Cache (one plane's
-// 1 MiB per team at a time, 64 planes in flight) instead of streaming from HBM (16 of the 2-pass form's
-// 36 B/px per iteration).  Same bodies as column_kernel / line_kernel, so the same results bit for bit.
-// Team barrier (cdna_hip_programming.md Guideline 16, counter form): every wave drains its stores, one lane
-// releases at agent scope, adds to the team's counter and polls it relaxed; one agent acquire after the
-// match.  Every spin is bounded: on a timeout the lane sets err[0] and every later wait of every team
-// returns at once, so the grid always drains (results are then invalid; the host reports the flag).
-__device__ __forceinline__ void team_barrier(unsigned* cnt, unsigned target, unsigned* err) {
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 22)) {   // ~0.5 s: a member is not resident
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-}
-
-constexpr int kTeamSize = 4, kTeamThreads = 1024, kTeamKB = 16, kTeamT = 16;
-__device__ unsigned g_team512_sync[1024];   // team counters + error word (experiment: one call at a time)
-
-// The two phases as real calls: inlined into the persistent loop, the compiler hoists loop-invariant work of both
-// bodies and the kernel spilled 196 B/lane at the 128-VGPR cap of 1024-thread workgroups (each phase alone: 0)
-__device__ __attribute__((noinline)) void team_column(XBlk xb, const float2* src, float2* dst, const float* Ct,
-                                                      const float2* twN, float cs) {
-    column_body<512, 0, false, false, kTeamThreads>(xb, src, dst, Ct, nullptr, twN, 256, kTeamKB, cs, nullptr, nullptr);
-}
-__device__ __attribute__((noinline)) void team_line(XBlk xb, const float2* spec1, float2* spec0, const float* so, float* sn,
-                                                    const float* hty, const float2* twM, const float* prm, int s_zero) {
-    line_body<256, kTeamT, kTeamThreads>(xb, spec1, spec0, so, sn, hty, twM, 512, prm, s_zero);
-}
-
-// grid = a multiple of 32 workgroups, all resident (cooperative launch); sync = nteams counters + err word, zeroed
-__global__ __launch_bounds__(kTeamThreads) void team512_kernel(const float2* first, float2* spec0, float2* spec1,
-                                                               float* sA, float* sB, const float* __restrict__ hty,
-                                                               const float* __restrict__ Ct, const float2* __restrict__ twM,
-                                                               const float2* __restrict__ twN, const float* __restrict__ prm,
-                                                               int planes, int K, float cs1, unsigned* sync) {
-    constexpr int NN = 512, L = 256;
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int x = b & 7, l = b >> 3;                 // XCD, slot on it
-    const int tpx = nwg / 8 / kTeamSize;             // teams per XCD
-    const int team = x * tpx + l / kTeamSize, member = l % kTeamSize;
-    const int nteams = nwg / kTeamSize;
-    unsigned* cnt = sync + team;
-    unsigned* err = sync + nteams;
-    unsigned target = 0;
-    constexpr int kColBlocks = L / kTeamKB / kTeamSize;   // 4 slot blocks of 16 per member
-    constexpr int kLineBlocks = NN / kTeamT / kTeamSize;  // 8 line blocks of 16 per member
-    for (int p = team; p < planes; p += nteams) {
-        for (int it = 1; it <= K; ++it) {
-            for (int c = 0; c < kColBlocks; ++c) {
-                team_column(XBlk{member * kColBlocks + c, p}, it == 1 ? first : spec0, spec1, Ct, twN, it == 1 ? cs1 : 1.0f);
-                __syncthreads();
-            }
-            target += kTeamSize;
-            team_barrier(cnt, target, err);
-            if (it == K) break;
-            float* so = (it & 1) ? sB : sA;   // iteration 1 reads nothing (s_zero)
-            float* sn = (it & 1) ? sA : sB;
-            for (int c = 0; c < kLineBlocks; ++c) {
-                team_line(XBlk{member * kLineBlocks + c, p}, spec1, spec0, so, sn, hty, twM, prm, it == 1 ? 1 : 0);
-                __syncthreads();
-            }
-            target += kTeamSize;
-            team_barrier(cnt, target, err);
-        }
-    }
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -92,34 +92,6 @@ int launch_line(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* s
     return -1;
 }
 
-// the persistent 512 x 512 team launch (admm_kernels.hip team512_kernel; experiment): every workgroup resident
-// (cooperative launch), whole teams of 4 per XCD, counters zeroed per call
-int launch_team512(hipStream_t s, const float2* first, float2* spec0, float2* spec1, float* sA, float* sB,
-                   const float* hty, const float* Ct, const float2* twM, const float2* twN, const float* prm, int planes,
-                   int K, float cs1) {
-    const size_t lds = std::max(line_lds(512, kTeamT), (size_t)512 * 16 + (size_t)kTeamKB * 513 * 8);
-    static int nwg = -1;
-    if (nwg < 0) {
-        set_lds(team512_kernel, lds);
-        int per = 0, dev = 0, cus = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, team512_kernel, kTeamThreads, lds) != hipSuccess) per = 0;
-        nwg = per * cus / (8 * kTeamSize) * (8 * kTeamSize);
-    }
-    if (nwg < 8 * kTeamSize) return fail(ADMM_E_UNSUPPORTED, "team512: no resident grid (%d workgroups)", nwg);
-    void* sync = nullptr;
-    hipError_t e = hipGetSymbolAddress(&sync, HIP_SYMBOL(g_team512_sync));
-    if (e == hipSuccess) e = hipMemsetAsync(sync, 0, (size_t)(nwg / kTeamSize + 1) * 4, s);
-    if (e != hipSuccess) return fail(ADMM_E_HIP, "team512 sync: %s", hipGetErrorString(e));
-    unsigned* sy = static_cast<unsigned*>(sync);
-    void* args[] = {&first, &spec0, &spec1, &sA, &sB, &hty, &Ct, &twM, &twN, &prm, &planes, &K, &cs1, &sy};
-    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(team512_kernel), dim3(nwg), dim3(kTeamThreads), args,
-                                   (unsigned)lds, s);
-    if (e != hipSuccess) return fail(ADMM_E_HIP, "team512 cooperative launch (%d workgroups): %s", nwg, hipGetErrorString(e));
-    return 0;
-}
-
 // planes: per branch; ngb: plane groups per branch (grid y = branches x ngb), 0: one branch
 int launch_iso_a(int L, int T, dim3 g, size_t lds, hipStream_t s, const float2* spec1, const float* so, float* sn,
                  const float* fmap, float* part, const float2* twM, int N, int planes, int G, int sz, int ngb = 0) {
@@ -310,8 +282,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         if (rc) return rc;
         rc = ln.run(ADMM_K_PLANE, [&] {
             return pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
-                                   planes, s, tr.m ? nullptr : reinterpret_cast<float4*>(tr.s),
-                                   fwd_stagger(), nullptr, tr.m);
+                                   planes, s, tr.m ? nullptr : reinterpret_cast<float4*>(tr.s), nullptr, tr.m);
         });
         return rc;
     }
@@ -359,14 +330,9 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     // them share a CU, admm_kernels.hip line_kernel); the one-off line transforms keep T
     // 512-point lines: 8-line update blocks of 512 threads (round 5, tools/c4_line_sweep.sh: line pass 1.217 ->
     // 1.196 ms at c4; 4 lines x 256 threads was round 1's choice; 16 x 1024, 4 x 512 and 8 x 1024 slower:
-    // profiles/r05_c4_line_sweep.jsonl).  ADMM_EXP_LINE512 = "T,threads" overrides (experiments)
-    int Tu = (M == 512 && T > 4) ? 8 : T;
-    int nTu = (M == 512 && Tu == 8) ? 512 : kThreads;
-    if (M == 512) {
-        static const char* e = getenv("ADMM_EXP_LINE512");
-        int et = 0, en = 0;
-        if (e && sscanf(e, "%d,%d", &et, &en) == 2 && et > 0 && en > 0) { Tu = et; nTu = en; }
-    }
+    // profiles/r05_c4_line_sweep.jsonl)
+    const int Tu = (M == 512 && T > 4) ? 8 : T;
+    const int nTu = (M == 512 && Tu == 8) ? 512 : kThreads;
     const size_t llds = line_lds(M, Tu), flds = fwdinv_lds(M, T), clds = column_lds(N, KB);
     float* fmap = iso ? reinterpret_cast<float*>(ws + lay.fmap) : nullptr;
     float* part = iso ? reinterpret_cast<float*>(ws + lay.part) : nullptr;
@@ -389,12 +355,9 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                                     twN, prm, maxit, tr, red);
         return ln.run(ADMM_K_PLANE, [&] {
             return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, np * 2 * MN, x_out, Ct, twM, twN, prm,
-                                    maxit, fwd_stagger());
+                                    maxit);
         });
     }
-    // experiment (round 5): the 512 x 512 anisotropic solve as one persistent team launch (team512_kernel)
-    static const bool team512 = getenv("ADMM_EXP_TEAM512") && atoi(getenv("ADMM_EXP_TEAM512")) > 0;
-    const bool use_team = team512 && M == 512 && N == 512 && !iso && !tr.s && !tr.v;
     // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
     rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
     if (rc) return rc;
@@ -409,13 +372,6 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         cs1 = (float)M;
     }
     const size_t sstride = np * 2 * MN;   // one trajectory slot of s
-    if (use_team) {
-        rc = ln.run(ADMM_K_PLANE, [&] {
-            return launch_team512(s, first, spec0, spec1, sbuf[0], sbuf[1], hty, Ct, twM, twN, prm, (int)np, maxit, cs1);
-        });
-        if (rc) return rc;
-        return ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
-    }
     for (int it = 1; it <= maxit; ++it) {
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * np * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
@@ -558,8 +514,7 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
                                 prm, maxit, tr, red);
     if (res) {
         return ln.run(ADMM_K_PLANE, [&] {
-            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit,
-                                    fwd_stagger());
+            return admm::rs::launch(M, N, planes, s, hty, sbuf[0], sbuf[1], tr.s, sstride, x_out, Ct, twM, twN, prm, maxit);
         });
     }
     for (int it = 1; it <= maxit; ++it) {
@@ -797,7 +752,7 @@ int launch_backward(int phases, const float* y, const float* x_bar, float* y_bar
         rc = ln.run(ADMM_K_ADJ, [&] {
             return pk::launch_plane_adj(x_bar, ws + bl.f.F, tr.m ? static_cast<const void*>(tr.m) : tr.s, dxK,
                                        reinterpret_cast<float4*>(sb[0]), specA, vout, rpart, prm, K, planes, s,
-                                       nullptr, tr.m != nullptr, adj_stagger());
+                                       nullptr, tr.m != nullptr);
         });
         if (rc) return rc;
         red_rows = (int)planes;
@@ -1336,8 +1291,7 @@ int launch_forward_multi(const float* y, float* x_out, int M, int N, int P, int 
     rc = ln.run(ADMM_K_PLANE, [&] {
         return admm::plane::launch_plane(y, x_out, ws + L.F, false, reinterpret_cast<float2*>(ws + L.hln),
                                          reinterpret_cast<float4*>(ws + L.sln), prm, maxit, planes, s,
-                                         rec && !masks ? reinterpret_cast<float4*>(ws + L.traj) : nullptr,
-                                         fwd_stagger(), &br,
+                                         rec && !masks ? reinterpret_cast<float4*>(ws + L.traj) : nullptr, &br,
                                          masks ? reinterpret_cast<unsigned*>(ws + L.traj) : nullptr);
     });
     if (rc) return rc;
@@ -1430,7 +1384,7 @@ int launch_backward_multi(const float* x_bar, float* y_bar, float* lambda_bar, f
     rc = ln.run(ADMM_K_ADJ, [&] {
         return admm::plane::launch_plane_adj(x_bar, ws + L.F, ws + L.traj, dxK, reinterpret_cast<float4*>(ws + L.sbar),
                                              reinterpret_cast<float2*>(ws + L.vsl), vbuf, part,
-                                             prm, K, planes, s, &br, masks, adj_stagger());
+                                             prm, K, planes, s, &br, masks);
     });
     if (rc) return rc;
     double* rt = reinterpret_cast<double*>(ws + L.rt);

@@ -24,14 +24,6 @@ int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 bool fused_enabled() { return opt(ADMM_OPT_FUSED) != 0; }
 // ADMM_OPT_FUSED_ADJ = 0 keeps the 2-pass reverse sweep (line_adj + column) on a fused trajectory
 bool fused_adj_enabled() { return opt(ADMM_OPT_FUSED_ADJ) != 0; }
-// Start stagger of the fused kernels (odd workgroups of the first wave start late, 10 ns ticks).  The reverse sweep
-// defaults to 35 us, about half a reverse step: its s-bar stream slows with the number of planes whose row phases
-// run together (120 planes 2.74 ms, 255 planes 3.50 ms per K = 50 sweep), and two phase groups take c5 at batch 17
-// 2.40k -> 2.52k img/s, at batch 64 2.43k -> 2.46k (profiles/r05_c5_sweep_stagger.jsonl).  The forward kernels
-// gain nothing from it and keep 0.
-constexpr int kAdjStagger = 3500;
-int fwd_stagger() { const int v = opt(ADMM_OPT_PLANE_STAGGER); return v > 0 ? v : 0; }
-int adj_stagger() { const int v = opt(ADMM_OPT_PLANE_STAGGER); return v < 0 ? 0 : v == 0 ? kAdjStagger : v; }
 
 // ---- tile-size policy ------------------------------------------------------------------------
 // T = lines per line-kernel block (power of two dividing N); KB = slots per column-kernel block.

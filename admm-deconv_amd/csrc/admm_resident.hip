@@ -794,11 +794,7 @@ __device__ __forceinline__ void line_chunk(float2 (&S)[NREG], const float2 (&hs)
         const int scr = 2 * G::BUF + w * 2 * MM;
         PV vf[QG], vl[QG];
         PV s0a[QG];   // RS_INPLACE: s channel 0 of the wave's first row, stored after the barrier
-#ifdef RS_SKIP_ROWS   // timing experiments only: no row update (wrong results)
-        if (false) {
-#else
         if (ub >= ua) {
-#endif
             PV w0c[QG];
             {
                 const int j = jc0 + ua - 2;
@@ -1103,15 +1099,8 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
                                                        float* __restrict__ sB, float* __restrict__ traj, size_t traj_stride,
                                                        float* __restrict__ x_all, const float* __restrict__ Ct,
                                                        const float2* __restrict__ twM, const float2* __restrict__ twN,
-                                                       const float* __restrict__ prm, int maxit, int stagger) {
+                                                       const float* __restrict__ prm, int maxit) {
     using G = Geo<MM, NN>;
-    // Phase groups (ADMM_OPT_PLANE_STAGGER): workgroup group g = (blockIdx / 8) % 4 starts g * stagger ticks of
-    // the 100 MHz realtime clock late, so that the groups' HBM-bound row updates do not all coincide
-    if (stagger > 0) {
-        const unsigned g = (blockIdx.x >> 3) & 3;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)g * (unsigned)stagger) __builtin_amdgcn_s_sleep(10);
-    }
     constexpr int NREG = G::NREG, NR = G::NR, NCC = G::NCC;
     constexpr size_t MN = (size_t)MM * NN;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1146,9 +1135,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
     static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kInit>(S, hs, th, la); });
 #pragma unroll 1
     for (int it = 1; it <= maxit; ++it) {
-#ifndef RS_SKIP_COL
         column_phase<MM, NN>(S, th, Ct);
-#endif
         if (it == maxit) {
             static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kFinal>(S, hs, th, la); });
             break;
@@ -1172,9 +1159,7 @@ __global__ __launch_bounds__(kNT) void resident_kernel(const float* __restrict__
 #pragma unroll
             for (int c = 0; c < NCC; ++c) hs[C * NCC + c] = S[c * NR + (C * G::TL - 2) / G::LS];
         });
-#ifndef RS_SKIP_UPD
         static_for<0, G::NLC>([&](auto ic) { line_chunk<MM, NN, decltype(ic)::value, kUpdate>(S, hs, th, la); });
-#endif
     }
 }
 
@@ -1316,14 +1301,14 @@ int launch_iso(int M, int N, size_t planes, hipStream_t s, const float* hty, con
 
 int launch(int M, int N, size_t planes, hipStream_t s, const float* hty, float* sA, float* sB, float* traj,
            size_t traj_stride, float* x_out, const float* Ct, const float2* twM, const float2* twN, const float* prm,
-           int maxit, int stagger) {
+           int maxit) {
 #define X(m, n)                                                                                                  \
     if (M == m && N == n) {                                                                                      \
         constexpr size_t lds = Geo<m, n>::lds_bytes();                                                           \
         (void)hipFuncSetAttribute((const void*)resident_kernel<m, n>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   (int)lds);                                                                     \
         resident_kernel<m, n><<<dim3((unsigned)planes), kNT, lds, s>>>(hty, sA, sB, traj, traj_stride, x_out, Ct, \
-                                                                        twM, twN, prm, maxit, stagger);          \
+                                                                        twM, twN, prm, maxit);                   \
         return 0;                                                                                                \
     }
     RS_SHAPES(X)

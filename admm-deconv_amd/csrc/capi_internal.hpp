@@ -30,8 +30,6 @@ int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int opt(int k);
 bool fused_enabled();
 bool fused_adj_enabled();
-int fwd_stagger();   // ADMM_OPT_PLANE_STAGGER for the forward per-plane kernels (default 0)
-int adj_stagger();   // ... for the fused 256^2 reverse sweep (default kAdjStagger)
 int line_T(int M, int N);
 size_t line_lds(int M, int T);
 size_t fwdinv_lds(int M, int T);

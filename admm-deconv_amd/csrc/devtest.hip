@@ -6,6 +6,7 @@
 #include "line_pair.hpp"
 #include "line_quad.hpp"
 #include "plane_kernel.hip"
+#include "capi_internal.hpp"
 
 namespace {
 
@@ -128,6 +129,17 @@ int devtest_recording_offsets(int M, int N, int P, int B, int kh, int maxit, int
         admm::layout::bwd_head(M, N, (size_t)P * B, kh, maxit, want_h != 0, iso != 0);
     *traj_s = b.traj_s;
     *traj_n = b.traj_n;
+    return 0;
+}
+// The reverse sweep's h_bar intermediates (tools/hbar_paths.py: which of h_bar's two cancelling paths carries
+// the error): byte offsets of Vsum (planes x M x N fp32), Q (fp64 (M/2+1) x N, after the plane sum), the path
+// through H^T y and the path through C (kh x kw fp64 each), from the library's own backward layout.
+int devtest_hbar_offsets(int M, int N, int P, int B, int kh, int kw, int maxit, size_t* out4) {
+    const admm_capi::BwdLayout b = admm_capi::make_bwd_layout(M, N, (size_t)P * B, kh, kw, maxit, true, false, false);
+    out4[0] = b.vsum;
+    out4[1] = b.Q;
+    out4[2] = b.hcorr;
+    out4[3] = b.hA;
     return 0;
 }
 // fused plane kernel (no PSF) with per-phase dumps of plane 0: dbg holds (4K) x 64 x 512 float2.

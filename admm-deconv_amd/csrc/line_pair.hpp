@@ -24,16 +24,9 @@ namespace admm {
 
 #include "tw256.inc"
 
-// Instruction-count trims (round 5 experiment switches, off): 1 = the lane-pair add / subtract as one FMA with the
-// lane's sign, 2 = lane exchanges pinned on the caller's variable (no v_mov copy), 4 = no select for iteration 1's
-// zero s (plane_kernel.hip row_update, plane_iso.hip row_iso_a).  All three cut the c2 iteration loop from 12.4k
-// to 11.6k VALU per wave (tools/isa_mix.py), yet each alone made c2 5 % SLOWER (164k -> 156-161k img/s, A/B on
-// one box, profiles/r05_plane_xv_ab.jsonl): the removed instructions were independent filler between dependent
-// ones at 2 waves per SIMD, and issue stalls rose (SQ_WAIT_INST_ANY 0.296 -> 0.334 of wave cycles,
-// profiles/r05_plane_xv_sq.json).  All three together: c5 +2 %.  The kernel is bound by dependency latency.
-#ifndef PLANE_XV
-#define PLANE_XV 0
-#endif
+// (Round 5 measured three instruction-count trims here -- FMA lane-pair add / subtract, exchanges pinned on the
+// caller's variable, no select for iteration 1's zero s: 12.4k -> 11.6k VALU per wave, yet c2 5 % slower,
+// profiles/r05_plane_xv_ab.jsonl.  They live on as tools/variants/plane_xv.patch, not in this source.)
 
 // v * W256^E (forward, W256 = exp(-2 pi i/256)) or v * conj(W256^E) (inverse)
 template <int E, bool INV>
@@ -76,13 +69,7 @@ __device__ __forceinline__ float2 swap_pair(float2 v) {
 // later uses read the same (pinned) registers -- pinning a by-value copy made the compiler keep the original
 // alive beside it (two v_mov per register of every lane-pair combine)
 __device__ __forceinline__ float2 swap_pair_keep(float2& v) {
-#if defined(ADMM_SWAP_BPERMUTE) || !(PLANE_XV & 2)
     return swap_pair(v);
-#else
-    __asm__ volatile("" : "+v"(v.x), "+v"(v.y));
-    return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), 0xB1, 0xF, 0xF, true)),
-                       __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), 0xB1, 0xF, 0xF, true)));
-#endif
 }
 
 // ---- in-register N-point FFT (N = 32 or 64), natural order in and out: N = 4 (n1) x N/4 (n2) -----
@@ -164,11 +151,7 @@ __device__ __forceinline__ void fft64_reg_stage(float2 (&x)[64], float2* stg, fl
 // instead of both results and a select per component.
 __device__ __forceinline__ float lane_sign(bool hb) { return hb ? -1.0f : 1.0f; }
 __device__ __forceinline__ float2 pm_pair(float2 mine, float2 oth, float sg) {
-#if PLANE_XV & 1
-    return make_float2(fmaf(mine.x, sg, oth.x), fmaf(mine.y, sg, oth.y));
-#else
     return sg < 0.0f ? csub(oth, mine) : cadd(mine, oth);
-#endif
 }
 
 // forward DIT combine across the pair: A: Z[k] = E[k] + W128^k O[k], B: Z[k+64] = E[k] - W128^k O[k]

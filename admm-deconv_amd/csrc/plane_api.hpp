@@ -51,14 +51,13 @@ hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStr
 // traj != NULL: record s_1..s_{K-1} for the adjoint, slot k-1 at traj + (k-1) * planes * 64 * 512
 // (lane-native: float4 (s0[p], s0[p+1], s1[p], s1[p+1]) of pixel pair p = 4n + 2h of line r at
 // [plane][n][2r + h]; s0 = x - x(line r-1), s1 = x - x(pixel p-1)); sln is then unused
-// prm: device {tau, rho, lambda} (setup_kernel); stagger: experiment option ADMM_OPT_PLANE_STAGGER (realtime
-// ticks of 10 ns that odd workgroups start late; 0 = off)
+// prm: device {tau, rho, lambda} (setup_kernel)
 // masks != NULL (and traj NULL): record only the ST mask bits of s_1..s_{K-1} (plane_kernel.hip mask_byte),
 // slot k-1 at masks + (k-1) * planes * 16 * 512 dwords, for a reverse sweep without rho_bar.
 // br (NULL = one solve): several branches in one grid; tables / prm then hold br->nbr consecutive blocks.
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
                         const float* prm, int K, size_t planes, hipStream_t s, float4* traj = nullptr,
-                        int stagger = 0, const Branches* br = nullptr, unsigned* masks = nullptr);
+                        const Branches* br = nullptr, unsigned* masks = nullptr);
 
 
 // Reverse sweep of the anisotropic solve on the fused trajectory (plane256_adj_kernel):
@@ -71,7 +70,7 @@ hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream
 // chcat layout; vout and part per grid plane).
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s, const Branches* br = nullptr, bool masks = false, int stagger = 0);
+                            hipStream_t s, const Branches* br = nullptr, bool masks = false);
 
 // Isotropic (BT) solve at 256 x 256 (plane_iso.hip): iteration k = 0 .. K-1 of every plane (hln: H^T y,
 // lane-native, written at k = 0; s_in / s_out: s_k / s_{k+1}, the same state buffer, or trajectory slots k-1 / k

@@ -95,9 +95,7 @@ __device__ __forceinline__ void row_iso_a(float2 (&S)[64], rsrc_t sld, rsrc_t ss
         // u_k = s_k - f s_k (z = f s, ops.jl:10), channel pairs (x, z) at pixel p and (y, w) at p + 1
         // (first: sld and fld are resources of size 0, so a = f = 0 and u = 0 without a select)
         float4 u = make_float4(a.x - f.x * a.x, a.y - f.y * a.y, a.z - f.x * a.z, a.w - f.y * a.w);
-#if !(PLANE_XV & 4)
         if (first) u = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
         const float4 s = make_float4((x.x - xu.x) + u.x, (x.y - xu.y) + u.y, (x.x - xl) + u.z, (x.y - x.x) + u.w);
         bst4(sst, t * 16, n * kPT * 16, s);
         bst2(qst, t * 8, n * kPT * 8, make_float2(s.x * s.x + s.z * s.z, s.y * s.y + s.w * s.w));

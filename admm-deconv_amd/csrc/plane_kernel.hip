@@ -239,10 +239,6 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     float2 gf[MODE == 1 ? 32 : 1];
 #pragma unroll
     for (int j = 0; j < NGF; ++j) {
-#ifdef PLANE_EXPT_NOCF
-        // timing experiment only (wrong results): no multiplier loads in the x-update column phase
-        if constexpr (MODE == 0) { cf[j] = 1.0f / 65536.0f; continue; }
-#endif
         if constexpr (MODE == 0) cf[j] = bld1(Cf, t * 4, (HALF * 32 + j) * kPT * 4);
         else gf[j] = bld2(Gf, t * 8, (HALF * 32 + j) * kPT * 8);
     }
@@ -340,11 +336,7 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
 // v is pinned in place (the caller's own variable, which it reads again): pinning a by-value copy kept the
 // original alive beside it, one v_mov per shift
 __device__ __forceinline__ float lane_up2(float& vr) {   // lane i <- lane i - 2
-#if PLANE_XV & 2
-    float& v = vr;
-#else
     float v = vr;
-#endif
 #if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true);
@@ -354,11 +346,7 @@ __device__ __forceinline__ float lane_up2(float& vr) {   // lane i <- lane i - 2
 #endif
 }
 __device__ __forceinline__ float lane_down2(float& vr) {   // lane i <- lane i + 2
-#if PLANE_XV & 2
-    float& v = vr;
-#else
     float v = vr;
-#endif
 #if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true);
@@ -463,11 +451,6 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
     for (int g = 0; g < NCH; ++g) {
         const int n0 = g * CH;
         if (g + PD < NCH) {
-#ifdef PLANE_VMEM_NOPS
-            // wait states between the last VALU/DPP reads and the loads that overwrite the slot
-            sched_fence();
-            __asm__ volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-#endif
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 // keep the slot's old value live up to here, so its registers are not recycled as
@@ -507,13 +490,9 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
             xu.y = top ? xub.y : xu.y;
             // iteration 1 (first): so comes from a resource of size 0 (the caller's), i.e. 0, and clip(0) = 0: no select
             float4 uo = make_float4(clip_tau(so.x, tau), clip_tau(so.y, tau), clip_tau(so.z, tau), clip_tau(so.w, tau));
-#if !(PLANE_XV & 4)
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
-#ifndef PLANE_EXPT_NOSTORE
             bst4<PLANE_AUX_ST>(sps, t * 16, n * kPT * 16, s);
-#endif
             if constexpr (MASK) {
                 mbits |= mask_byte(s, tau) << (8 * (n & 3));
                 if ((n & 3) == 3) {
@@ -581,12 +560,6 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
     }
 }
 
-// timing experiments only (wrong results): skip the column phases (1), the line transforms (2) or the
-// row update (4) of every iteration
-#ifndef PLANE_EXPT_SKIP
-#define PLANE_EXPT_SKIP 0
-#endif
-
 #ifndef PLANE_STAGE_INV
 #define PLANE_STAGE_INV 1
 #endif
@@ -602,7 +575,7 @@ template <bool PSF, int DBG = 0, int TRAJ = 0>
 __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__ y, float* __restrict__ x_out,
                                                        const float* __restrict__ Cf, const float* __restrict__ C0b,
                                                        const float2* __restrict__ Gf, const float2* __restrict__ G0b,
-                                                       float2* __restrict__ hln, float4* __restrict__ sln, const float* __restrict__ prm, int K, float2* dbg = nullptr, int stagger_ticks = 0,
+                                                       float2* __restrict__ hln, float4* __restrict__ sln, const float* __restrict__ prm, int K, float2* dbg = nullptr,
                                                        float4* __restrict__ traj = nullptr, size_t traj_slot = 0,
                                                        Branches br = Branches{1, 1, 1, 0u, 0u},
                                                        unsigned* __restrict__ mtraj = nullptr, size_t mslot = 0) {
@@ -613,15 +586,9 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     G0b = reinterpret_cast<const float2*>(reinterpret_cast<const float*>(G0b) + (size_t)bo.i * br.tab_f);
     prm += (size_t)bo.i * br.prm_f;
     const float tau = prm[0]; const float rho = prm[1];   // device-resident scalars (setup_kernel)
-    // Phase stagger: workgroups with odd index start `stagger_ticks` of the 100 MHz realtime clock
-    // late, so that the memory-heavy row phases of two groups of CUs interleave.
     if constexpr (DBG >= 2) {   // workgroup start / end on the constant 100 MHz clock (slots 508 / 509 of wave 0)
         if (threadIdx.x == 0)
             reinterpret_cast<unsigned long long*>(dbg)[(size_t)blockIdx.x * 8 * 512 + 508] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (stagger_ticks > 0 && (blockIdx.x & 1)) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)stagger_ticks) __builtin_amdgcn_s_sleep(10);
     }
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     float2* colbuf = reinterpret_cast<float2*>(smem_raw);
@@ -667,11 +634,9 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     line_forward_pair(S, hb);
     dbg_dump<DBG>(dbg, S, 0, t);
     for (int k = 1;; ++k) {
-        if constexpr (!(PLANE_EXPT_SKIP & 1)) {
         column_half<0, 0>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
         if constexpr (DBG == 2) dbg_dump<DBG>(dbg, S, 256 + k, t);
         column_half<0, 1>(S, colbuf, tw, mir, cfr, c0l, gfr, G0b, t, hb);
-        }
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
         // the last iteration keeps x in registers for the output; the others hand x[32..63] to the
         // row phase's LDS staging slots directly (no spill of the line inverse's peak)
@@ -681,12 +646,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
             dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
             if (k == K) break;
         } else {
-            if constexpr (PLANE_EXPT_SKIP & 2) {
-#pragma unroll
-                for (int m = 0; m < 32; ++m) colbuf[t + m * kPT] = S[32 + m];
-            } else {
-                line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
-            }
+            line_inverse_pair_staged(S, hb, colbuf + t, colbuf + t + 16 * kPT);
             if (k == K) {   // the output needs x[32..63] back (per-thread slots: no barrier)
 #pragma unroll
                 for (int m = 0; m < 16; ++m) S[32 + m] = colbuf[t + m * kPT];
@@ -712,15 +672,10 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
             // ... and s_{K-1} is never read (iteration K stops at x): its stores drop the same way
             const rsrc_t sld = k >= 2 ? sp : make_rsrc(sln, 0);
             const rsrc_t sst = k <= K - 2 ? sp : make_rsrc(sln, 0);
-            if constexpr (PLANE_EXPT_SKIP & 4) {
-#pragma unroll
-                for (int m = 0; m < 32; ++m) S[32 + m] = colbuf[t + m * kPT];
-            } else {
-                row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho, sld);
-            }
+            row_update<kStage>(S, sld, sst, hp, xb, wb, sink, colbuf, t, hb, k == 1, tau, rho, sld);
         }
         dbg_dump<DBG>(dbg, S, 4 * k - 1, t);
-        if constexpr (!(PLANE_EXPT_SKIP & 2)) line_forward_pair(S, hb);
+        line_forward_pair(S, hb);
         dbg_dump<DBG>(dbg, S, 4 * k, t);
     }
     float2* xrow = reinterpret_cast<float2*>(x_out + bo.out_plane * 65536 + (size_t)r * 256);
@@ -754,9 +709,6 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
 //   rho_acc += <phi(s_{k-1}), Dvb>,  tau_acc += m sgn(s_{k-1}) (sbar_k - 2 wbar);
 //   S <- g_{k-1} = D^T sbar_{k-1}  (finalize with H^T y = 0 and unit weight).
 // Chunks of ONE register (the ring holds 3 float4 + 1 float2 per register, 2.3x row_update's).
-#ifndef ADJX
-#define ADJX 0
-#endif
 // WV: the running sum Vsum of vbar is kept (y_bar or h_bar wanted); without it no Vsum instruction is issued
 // at all (zero-size resources would drop the traffic, but their loads still queue in the in-order vmcnt)
 template <bool MASK, bool WV>
@@ -818,10 +770,10 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
             }
             __asm__ volatile("" ::"v"(sbr[q].x), "v"(sbr[q].y), "v"(sbr[q].z), "v"(sbr[q].w));
             if constexpr (WV) __asm__ volatile("" ::"v"(vr[q].x), "v"(vr[q].y));
-            if (!MASK && !(ADJX & 8)) s1r[q] = bld4(s1p, t * 16, (n + PD) * kPT * 16);
-            if (!MASK && !(ADJX & 8)) s2r[q] = bld4(s2p, t * 16, (n + PD) * kPT * 16);
-            if (!(ADJX & 4)) sbr[q] = bld4(sbl, t * 16, (n + PD) * kPT * 16);
-            if (WV && !(ADJX & 2)) vr[q] = bld2(vlp, t * 8, (n + PD) * kPT * 8);
+            if (!MASK) s1r[q] = bld4(s1p, t * 16, (n + PD) * kPT * 16);
+            if (!MASK) s2r[q] = bld4(s2p, t * 16, (n + PD) * kPT * 16);
+            sbr[q] = bld4(sbl, t * 16, (n + PD) * kPT * 16);
+            if (WV) vr[q] = bld2(vlp, t * 8, (n + PD) * kPT * 8);
         }
         if (n == 32) {   // half-way: vbar[32..63] in, g[0..30] out (vbar[31] still pending in S[31])
 #pragma unroll
@@ -889,7 +841,7 @@ __device__ __forceinline__ void row_adjoint(float2 (&S)[64], rsrc_t s1p, rsrc_t 
         // pin the accumulators here: left free, the compiler sinks the sums to the end of the
         // unrolled loop and keeps every register's operands live until then (~2000 VGPRs of spills)
         __asm__ volatile("" : "+v"(racc), "+v"(tacc));
-        if (WV && !(ADJX & 2)) bst2(vsp, vso, n * vss, make_float2(vo.x + v.x, vo.y + v.y));
+        if (WV) bst2(vsp, vso, n * vss, make_float2(vo.x + v.x, vo.y + v.y));
         const float4 nb4 = make_float4(nb[0], nb[1], nb[2], nb[3]);
         bst4(sbs, t * 16, n * kPT * 16, nb4);
         wbm[n] = make_float2(nb4.x, nb4.y);
@@ -947,18 +899,7 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
                                                            const float4* __restrict__ dxK, float4* __restrict__ sbar,
                                                            float2* __restrict__ vsl, float* __restrict__ vout,
                                                            double* __restrict__ part, const float* __restrict__ prm, int K,
-                                                           Branches br, int stagger_ticks) {
-    // Phase stagger (experiment option ADMM_OPT_PLANE_STAGGER): odd workgroups of the first wave start
-    // `stagger_ticks` of the 100 MHz realtime clock late, so that two CU groups' row phases alternate.
-#ifndef ADJ_STAGGER_GROUPS
-#define ADJ_STAGGER_GROUPS 2   // phase groups of the first wave: group g = blockIdx mod G starts g / (G - 1) x stagger late
-#endif
-    constexpr unsigned kSG = ADJ_STAGGER_GROUPS;
-    if (stagger_ticks > 0 && (blockIdx.x % kSG) && blockIdx.x < 256) {
-        const unsigned long long d = (unsigned long long)stagger_ticks * (blockIdx.x % kSG) / (kSG - 1);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(10);
-    }
+                                                           Branches br) {
     const BranchOf bo = branch_of(br, blockIdx.x);
     Cf += (size_t)bo.i * br.tab_f;
     C0b += (size_t)bo.i * br.tab_f;
@@ -1016,10 +957,8 @@ __global__ __launch_bounds__(kPT) void plane256_adj_kernel(const float* __restri
         const unsigned vso = k >= 2 ? (unsigned)t * 8 : (unsigned)(r * 1024 + hb * 8);
         const unsigned vss = k >= 2 ? kPT * 8 : 16;
         float racc = 0.0f, tacc = 0.0f;
-#if !(ADJX & 1)
         row_adjoint<MASK, WV>(S, s1p, s2p, sbl, sbs, vlr, vsr, vso, vss, xb, wb, sink, colbuf, t, hb, k == K, tau, rho, racc,
                     tacc);
-#endif
         rsum += racc;
         tsum += tacc;
         if (k == 1) break;

@@ -35,24 +35,24 @@ static Branches one_branch() { return Branches{1, 1, 1, 0u, 0u}; }
 
 template <bool PSF, int TRAJ>
 static void launch_one(const float* y, float* x_out, const Tables& t, float2* hln, float4* sln, const float* prm,
-                       int K, size_t planes, hipStream_t s, int stagger, float4* traj, const Branches& br,
+                       int K, size_t planes, hipStream_t s, float4* traj, const Branches& br,
                        unsigned* masks) {
     (void)hipFuncSetAttribute((const void*)plane256_kernel<PSF, 0, TRAJ>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kLdsBytes);
     hipLaunchKernelGGL((plane256_kernel<PSF, 0, TRAJ>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s, y, x_out,
-                       t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, prm, K, nullptr, stagger, traj,
+                       t.Cf, t.C0b, t.Gf, t.G0b, hln, sln, prm, K, nullptr, traj,
                        planes * 64 * kPT, br, masks, planes * 16 * kPT);
 }
 
 hipError_t launch_plane(const float* y, float* x_out, const void* tables, bool psf, float2* hln, float4* sln,
-                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj, int stagger,
+                        const float* prm, int K, size_t planes, hipStream_t s, float4* traj,
                         const Branches* brp, unsigned* masks) {
     const Tables t = carve(tables);
     const Branches br = brp ? *brp : one_branch();
     const int mode = traj ? 1 : masks ? 2 : 0;
 #define X(P, M)                                                                                     \
     if (psf == P && mode == M) {                                                                    \
-        launch_one<P, M>(y, x_out, t, hln, sln, prm, K, planes, s, stagger, traj, br, masks);       \
+        launch_one<P, M>(y, x_out, t, hln, sln, prm, K, planes, s, traj, br, masks);               \
         return hipGetLastError();                                                                   \
     }
     X(false, 0) X(false, 1) X(false, 2) X(true, 0) X(true, 1) X(true, 2)
@@ -69,7 +69,7 @@ hipError_t launch_dx_lane(const float* xK, float4* dxK, size_t planes, hipStream
 
 hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* traj, const float4* dxK, float4* sbar,
                             float2* vsl, float* vout, double* part, const float* prm, int K, size_t planes,
-                            hipStream_t s, const Branches* brp, bool masks, int stagger) {
+                            hipStream_t s, const Branches* brp, bool masks) {
     const Tables t = carve(tables);
     const Branches br = brp ? *brp : one_branch();
     if (masks && dxK) return hipErrorInvalidValue;   // rho_bar needs the full trajectory
@@ -79,7 +79,7 @@ hipError_t launch_plane_adj(const float* xbar, const void* tables, const void* t
         (void)hipFuncSetAttribute((const void*)plane256_adj_kernel<MK, WV>,                                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);                \
         hipLaunchKernelGGL((plane256_adj_kernel<MK, WV>), dim3((unsigned)planes), dim3(kPT), kLdsBytes, s,    \
-                           xbar, t.Cf, t.C0b, traj, slot, dxK, sbar, vsl, vout, part, prm, K, br, stagger);         \
+                           xbar, t.Cf, t.C0b, traj, slot, dxK, sbar, vsl, vout, part, prm, K, br);                 \
     }
     X(false, false) X(false, true) X(true, false) X(true, true)
 #undef X

@@ -16,11 +16,10 @@ bool has_shape(int M, int N, bool all = false);
 bool has_iso_shape(int M, int N, bool all = false);
 // hty: H^T y per plane (or y itself without a PSF); s ping-pong buffers sA / sB ([plane][2][N][M]) unless
 // traj != nullptr (then s_k goes to traj + (k - 1) * traj_stride, read back from the previous slot);
-// Ct / twM / twN / prm: the setup kernel's tables; stagger: start delay per workgroup group (realtime ticks,
-// ADMM_OPT_PLANE_STAGGER).  Returns -1 when the shape is not compiled.
+// Ct / twM / twN / prm: the setup kernel's tables.  Returns -1 when the shape is not compiled.
 int launch(int M, int N, size_t planes, hipStream_t s, const float* hty, float* sA, float* sB, float* traj,
            size_t traj_stride, float* x_out, const float* Ct, const float2* twM, const float2* twN, const float* prm,
-           int maxit, int stagger = 0);
+           int maxit);
 
 // The isotropic solve's iteration k (0 .. K-1) as one launch (admm_resident.hip resident_iso_kernel): reads s_k
 // (s_in, k > 0) and f_k (fmap, M x N), writes s_{k+1} (s_out; may equal s_in) and q = s1^2 + s2^2 per plane

@@ -250,7 +250,7 @@ def bench_c5(args, dev):
         roof = {"bound": "hbm", "kernel": f"{dom} (2-pass {'isotropic ' if args.iso else ''}kernels, one grid of {nb} "
                                           f"branches x {planes} planes)",
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("c5iso2m", dom) if (B == 2 and args.iso) else None,
+                "traffic": load_traffic("c5iso2m", dom, planes=nb * planes) if args.iso else None,
                 "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(a["avg_ms"], 5)}
     elif merged and args.iso:
         # one grid of 5 x 192 planes per iteration / reverse step (plane_iso.hip, ADMM_MULTI_ISO)
@@ -267,7 +267,7 @@ def bench_c5(args, dev):
         roof = {"bound": "hbm", "kernel": f"{dom} (plane_iso.hip, one grid of {nb} branches x {planes} planes, "
                                           f"{K} launches)", "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("c5isom", dom), "algorithmic_bytes_per_launch": per[dom],
+                "traffic": load_traffic("c5isom", dom, planes=nb * planes), "algorithmic_bytes_per_launch": per[dom],
                 "avg_launch_ms": round(a["avg_ms"], 5)}
     elif merged:
         # one grid of 5 x 192 planes for the forward (plane256_kernel recording ST mask bits: lambda is the
@@ -288,7 +288,7 @@ def bench_c5(args, dev):
         ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": f"{dom} (one grid of {nb} branches x {planes} planes)", "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("c5m", dom), "algorithmic_bytes_per_launch": per[dom],
+                "traffic": load_traffic("c5m", dom, planes=nb * planes), "algorithmic_bytes_per_launch": per[dom],
                 "avg_launch_ms": round(a["avg_ms"], 5)}
     elif args.iso and kernels.get("plane", {}).get("launches_per_step") == len(branch) * K:
         # isotropic at 256 x 256: the split-iteration kernels of plane_iso.hip, one plane256_iso_kernel per
@@ -306,7 +306,7 @@ def bench_c5(args, dev):
         ach = per[dom] / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": f"{dom} (plane_iso.hip, {nb} branches x {K} launches)", "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("c5iso", dom), "algorithmic_bytes_per_launch": per[dom],
+                "traffic": load_traffic("c5iso", dom, planes=planes), "algorithmic_bytes_per_launch": per[dom],
                 "avg_launch_ms": round(a["avg_ms"], 5)}
     elif not args.iso and kernels.get("adjoint", {}).get("launches_per_step") == len(branch):
         # fused reverse sweep (plane256_adj_kernel, one launch per layer).  The input and rho need no gradient,
@@ -317,7 +317,7 @@ def bench_c5(args, dev):
         a = kernels["adjoint"]
         ach = per_launch / (a["avg_ms"] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "adjoint (plane256_adj)", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("c5", "adjoint"),
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("c5", "adjoint", planes=planes),
                 "algorithmic_bytes_per_launch": per_launch, "avg_launch_ms": round(a["avg_ms"], 5)}
     elif not args.iso and "adjoint" in kernels:
         # line_adj per plane and reverse step: packed line spectrum in + out (8 (M/2) N each), s_{k-1},
@@ -367,14 +367,19 @@ def cpu_baseline(cfg, psf, base, target_s):
     }
 
 
-def load_traffic(cfg_name, kernel, key="hbm_bytes_per_launch"):
+def load_traffic(cfg_name, kernel, key="hbm_bytes_per_launch", planes=None):
+    """A PMC figure per launch from profiles/pmc_traffic.json, or None.  The profiled launch's plane count is
+    recorded with it ("planes"): a launch over another number of planes gets None, not the profiled bytes (a
+    committed profile describes the launch it measured, not this one)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         e = d.get(cfg_name, {}).get(kernel)
-        return None if e is None else e.get(key)
+        if e is None or (planes is not None and e.get("planes") != planes):
+            return None
+        return e.get(key)
     except Exception:
         return None
 
@@ -384,17 +389,17 @@ def load_traffic(cfg_name, kernel, key="hbm_bytes_per_launch"):
 VALU_ISSUE_PEAK = 256 * 2 * 2.4e9   # wave-instructions per second
 
 
-def compute_side(cfg_name, kernel, avg_ms):
+def compute_side(cfg_name, kernel, avg_ms, planes):
     """Compute-side figure of the dominant kernel: SQ_INSTS_VALU per launch (PMC, profiles/pmc_traffic.json)
-    over the chip's VALU issue peak for the measured launch time."""
-    valu = load_traffic(cfg_name, kernel, "valu_insts_per_launch")
+    over the chip's VALU issue peak for the measured launch time (None off the profiled plane count)."""
+    valu = load_traffic(cfg_name, kernel, "valu_insts_per_launch", planes)
     if not valu:
         return None
     rate = valu / (avg_ms * 1e-3)
     return {"valu_insts_per_launch": valu, "valu_issue_rate": rate, "valu_issue_peak": VALU_ISSUE_PEAK,
             "valu_issue_frac": round(rate / VALU_ISSUE_PEAK, 4),
-            "lds_insts_per_launch": load_traffic(cfg_name, kernel, "lds_insts_per_launch"),
-            "wait_any_frac": load_traffic(cfg_name, kernel, "wait_any_frac")}
+            "lds_insts_per_launch": load_traffic(cfg_name, kernel, "lds_insts_per_launch", planes),
+            "wait_any_frac": load_traffic(cfg_name, kernel, "wait_any_frac", planes)}
 
 
 def spawn_ranks(n):
@@ -568,7 +573,7 @@ def main():
         kernels[name] = e
     dom = max((k for k in kernels if k in kb), key=lambda k: kernels[k]["total_ms_per_solve"])
     alg_bytes = kb["plane"] * planes if "plane" in kernels else canonical_bytes(M, N, K) * planes
-    traffic = load_traffic(config, dom)
+    traffic = load_traffic(config, dom, planes=planes)
     ach = kernels[dom]["achieved_GBps"]
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -578,7 +583,7 @@ def main():
         "frac_of_achievable": round(ach / achievable_gbs(), 4) if achievable_gbs() else None,
         "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
         "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
-        "compute": compute_side(config, dom, kernels[dom]["avg_ms"]),
+        "compute": compute_side(config, dom, kernels[dom]["avg_ms"], planes),
         "whole_solve": {
             # the bytes of the path that ran (fused: plane_bytes_per_px; 2-pass: SURVEY s8d canonical)
             "algorithmic_bytes": alg_bytes,

@@ -116,7 +116,8 @@ int admm_tvd_backward_f32(const float* y, const float* x_bar, float* y_bar, floa
  * With iso == 0 the reducer is ignored (planes are independent).  reducer == NULL (or fn == NULL)
  * is the unsharded call, identical to admm_tvd_forward_f32 / admm_tvd_backward_f32.  A sharded
  * isotropic call ignores the plane-count rule (ADMM_OPT_MIN_PLANES): every shard takes the per-plane
- * kernels whatever its own size, so that all shards hand the reducer their maps in one layout. */
+ * kernels whatever its own size, so that all shards hand the reducer their maps in one layout.  A recording
+ * remembers whether it was made with a reducer: its replay must pass one too (or none), else ADMM_E_INVALID. */
 typedef int (*admm_reduce_fn)(float* buf, size_t count, void* stream, void* user);
 typedef struct {
     admm_reduce_fn fn;
@@ -240,9 +241,8 @@ enum {
     ADMM_OPT_COL_THREADS = 3,    /* 0 (default): policy; 256, 512 or 1024 threads per column block       */
     ADMM_OPT_GEN_TM = 4,         /* 0 (default 2048): runtime-length line block points, 256..8192        */
     ADMM_OPT_GEN_KN = 5,         /* 0 (default 1024): runtime-length column block points, 256..8192      */
-    ADMM_OPT_PLANE_STAGGER = 6,  /* fused kernels' odd-workgroup start delay, 10 ns ticks: 0 (default):
-                                    none in the forward kernels, 3500 in the 256^2 reverse sweep; > 0: that
-                                    delay in both; -1: none anywhere                                       */
+    ADMM_OPT_PLANE_STAGGER = 6,  /* retired (round 6): the start-delay experiment left the kernels; the value
+                                    is still stored and read back, and changes nothing                     */
     ADMM_OPT_SMOOTH = 7,         /* 1 (default): compile-time-plan kernels for the listed non-power-of-two
                                     lengths (admm_smooth.hip); 0: runtime plans for every such shape;
                                     2 / 3: compiled, column plans forced increasing / decreasing (sweeps)  */
@@ -265,7 +265,8 @@ int admm_get_option(int option, int* value);
  * mode: ADMM_MODE_FORWARD (admm_tvd_forward_*), ADMM_MODE_RECORD (admm_tvd_forward_record_*; flags =
  * its ADMM_REC_* word; its replay runs the sweep returned here), ADMM_MODE_BACKWARD (admm_tvd_backward_*;
  * want_hbar / want_rho = h_bar / rho_bar non-NULL).  kh = 0: no PSF.  planes = P * B of the call (0: not known,
- * no plane-count rule, see ADMM_OPT_MIN_PLANES).  *fwd_path = the forward's ADMM_PATH_*,
+ * no plane-count rule, see ADMM_OPT_MIN_PLANES; a sharded call -- a batch reducer given -- is planned as planes = 0,
+ * so query it with 0).  *fwd_path = the forward's ADMM_PATH_*,
  * *bwd_path = the reverse sweep's ADMM_PATH_SWEEP_* (0 for a plain forward).  The current library options
  * (admm_set_option) are taken into account; no GPU is touched.  The multi-branch entry points are not
  * covered (one grid of the fused kernels, or ADMM_E_UNSUPPORTED). */

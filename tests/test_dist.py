@@ -105,3 +105,15 @@ def test_pipelined_shard_gather(world, n_local, chunks):
     assert len(calls) == 2 * min(chunks, n_local) and sum(calls) == 2 * n_local   # chunks capped at the shard
     ref = _solve(torch.from_numpy(synth.make_batch(world * n_local, M, N, PSF))).numpy()
     assert np.array_equal(got, ref)
+
+
+def test_shard_gather_refuses_steps_after_close():
+    """a closed ShardGather (single process, CPU) refuses further steps instead of copying into
+    released buffers."""
+    y = torch.zeros(2, 1, 8, 8)
+    sg = parallel.ShardGather(y, lambda ys, xs: xs.copy_(ys + 1))
+    sg.step()
+    assert torch.equal(sg.local(), torch.ones_like(y))
+    sg.close()
+    with pytest.raises(RuntimeError):
+        sg.step()

@@ -178,6 +178,17 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
         frac = assert_prox_active(mask_fraction(masks), cid, cid in LINEAR_ONLY)
         yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt, need_rho=need_rho)
         torch.cuda.synchronize()
+    return compare_to_oracle(cid, y, xbar, h, lam, rho, K, iso, masks, frac, x.cpu().numpy(), yb.cpu().numpy(),
+                             None if hb is None else hb.cpu().numpy(), float(lb), None if rb is None else float(rb),
+                             unconditioned=unconditioned)
+
+
+def compare_to_oracle(cid, y, xbar, h, lam, rho, K, iso, masks, frac, x, yb, hb, lb, rb, unconditioned=False):
+    """Errors of a GPU forward + adjoint (host arrays; rb None: rho_bar not formed) against the fp64 oracle
+    conditioned on `masks` (the GPU trajectory's own prox branches), and of an fp32 torch evaluation of the same
+    mask-conditioned computation (the arithmetic reference).  Also used for sharded batches
+    (test_gpu_dist_iso.py), whose masks come from the shards' common batch norms."""
+    need_rho = rb is not None
     lam32, rho32 = np.float32(lam), np.float32(rho)
     h64 = None if h is None else h.astype(np.float64)
     sc = {}
@@ -193,21 +204,19 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
     x32, yb32, hb32, lb32, rb32 = oracle_torch.tvd_fft_grads(y, lam32, rho32, h, iso, K, xbar, dtype=torch.float32,
                                                              masks=masks)
     info = {}
-    err = {"x": _plane_rel(x.cpu().numpy(), x0), "y_bar": _plane_rel(yb.cpu().numpy(), yb0),
+    err = {"x": _plane_rel(x, x0), "y_bar": _plane_rel(yb, yb0),
            "lambda_bar": abs(float(lb) - lb0) / max(lam_scale, 1e-300)}
     if need_rho:
         err["rho_bar"] = abs(float(rb) - rb0) / max(rho_scale, 1e-300)
-    else:
-        assert rb is None
     ref32 = {"x": _plane_rel(x32, x0), "y_bar": _plane_rel(yb32, yb0), "lambda_bar": abs(lb32 - lb0) / max(lam_scale, 1e-300),
              "rho_bar": abs(rb32 - rb0) / max(rho_scale, 1e-300)}
     if hb is not None:
         # h_bar = (its path through H^T y) + (its path through C), and the two cancel (factor ~2.7): the error is
         # measured against the sum of their absolute values, as lambda_bar / rho_bar against their terms
         h_scale = max(float(np.linalg.norm(sc["h"])), float(np.linalg.norm(hb0)), 1e-300)
-        err["h_bar"] = float(np.linalg.norm(np.asarray(hb.cpu().numpy(), np.float64) - hb0)) / h_scale
+        err["h_bar"] = float(np.linalg.norm(np.asarray(hb, np.float64) - hb0)) / h_scale
         ref32["h_bar"] = float(np.linalg.norm(np.asarray(hb32, np.float64) - hb0)) / h_scale
-        info["h_bar_rel_to_value"] = _rel(hb.cpu().numpy(), hb0)
+        info["h_bar_rel_to_value"] = _rel(hb, hb0)
     if cid not in LINEAR_ONLY:
         # tau enters the output only through live prox branches: a live case has lambda_bar != 0 on both sides
         assert lb0 != 0.0 and float(lb) != 0.0, f"{cid}: lambda_bar is zero with {frac:.2%} of the prox live"
@@ -227,10 +236,10 @@ def run_case(dev, cid, y, xbar, h, lam, rho, K, iso, need_h, opts, unconditioned
                                                      for a, b in zip(masks, own)))
     if unconditioned:
         _, ybu, hbu, lbu, rbu = oracle_torch.tvd_fft_grads(y.astype(np.float64), lam32, rho32, h64, iso, K, xbar)
-        info["unconditioned"] = {"y_bar": _plane_rel(yb.cpu().numpy(), ybu), "lambda_bar": _scalar_rel(float(lb), lbu),
+        info["unconditioned"] = {"y_bar": _plane_rel(yb, ybu), "lambda_bar": _scalar_rel(float(lb), lbu),
                                  "rho_bar": _scalar_rel(float(rb), rbu) if need_rho else None}
         if hb is not None:
-            info["unconditioned"]["h_bar"] = _rel(hb.cpu().numpy(), hbu)
+            info["unconditioned"]["h_bar"] = _rel(hb, hbu)
     out = os.environ.get("ADMM_GRAD_LOG")
     if out:
         with open(os.path.join(REPO, out), "a") as f:

@@ -262,6 +262,53 @@ def test_ipc_step_requires_gathered_unless_stream_only(dev, stream_only):
     assert all(r[1] is (not stream_only) for r in res), res
 
 
+def _close_worker(rank, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        y = torch.full((4, 1, 512, 512), float(rank + 1), device=dev)
+        sg = parallel.ShardGather(y, lambda ys, xs: xs.copy_(ys), engine="ipc", stream_only=True)
+        assert sg.engine == "ipc"
+        sg.step()
+        sg.close()   # rank 1: its peer copy may still be in flight -- close() drains the comm stream first
+        dist.barrier()
+        ok = True
+        if rank == 0:
+            torch.cuda.synchronize(dev)
+            got = sg.recv[0]
+            ok = bool((got[:4] == 1.0).all()) and bool((got[4:] == 2.0).all())
+        try:
+            sg.step()
+            raised = False
+        except RuntimeError:
+            raised = True
+        q.put((rank, ok and raised and sg.remote is None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_ipc_close_after_stream_only_step(dev):
+    """close() right after a stream_only step (nothing waited for the peer copy) drains the copy
+    stream before unmapping -- rank 0's buffer holds both shards -- and a later step() raises instead of copying
+    to an unmapped address."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_close_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True for r in res), res
+
+
 def test_copy_async_is_a_stream_ordered_device_copy(dev):
     """admm_copy_async (the IPC gather's peer copy, include/admm_deconv.h): a hipMemcpyAsync on the given stream,
     ordered after earlier work on that stream and before later work; NULL pointers are rejected; 0 bytes is a

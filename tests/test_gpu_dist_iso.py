@@ -29,7 +29,30 @@ def _inputs(M, nb=B):
     return h, y, xbar
 
 
+def _lane_native(M, need_rho):
+    """Whether the isotropic recording keeps s / |s| lane-native (the fused 256^2 sweep, recorded without rho_bar;
+    with rho_bar the PSF's h_bar trajectory takes the 2-pass layout) -- test_gpu_adjoint_masked.run_case's rule."""
+    from admm_deconv import _lib
+    return M == 256 and not need_rho and _lib.get_option("FUSED") == 1 and _lib.get_option("FUSED_ADJ") == 1
+
+
+def _record_and_replay(y, xbar, h, need_rho, dev, group=None):
+    """Forward recorded (sharded with `group`), its batch norms |s_1..s_{K-1}| read back, then the replay:
+    (x, |s_k| maps (K-1, M, M), y_bar, h_bar, lam_bar, rho_bar) as host values."""
+    import test_gpu_adjoint_masked as tm
+    yt, xt, ht = (torch.from_numpy(a).to(dev) for a in (y, xbar, h))
+    x, rec = admm_deconv.tvd_fft_record(yt, LAM, RHO, ht, True, K, need_h=need_rho, need_rho=need_rho, group=group)
+    torch.cuda.synchronize()
+    _, nrm = tm.read_trajectory(rec, K, _lane_native(y.shape[-1], need_rho))
+    yb, hb, lb, rb = admm_deconv.tvd_fft_backward_recorded(rec, x, xt, need_rho=need_rho)
+    torch.cuda.synchronize()
+    return (x.cpu().numpy(), np.array(nrm), yb.cpu().numpy(), None if hb is None else hb.cpu().numpy(), float(lb),
+            None if rb is None else float(rb))
+
+
 def _worker(rank, world, port, q, M, need_rho, resident=0, nb=B, min_planes=0):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from admm_deconv import _lib
     _lib.set_option("RESIDENT", resident if resident else 1)
@@ -49,8 +72,9 @@ def _worker(rank, world, port, q, M, need_rho, resident=0, nb=B, min_planes=0):
     x2, yb, hb, lb, rb = admm_deconv.tvd_fft_backward(ys, xb, LAM, RHO, ht, True, K, group=g, need_h=need_rho,
                                                       need_rho=need_rho)
     torch.cuda.synchronize()
+    rec = _record_and_replay(y[start:start + count], xbar[start:start + count], h, need_rho, dev, group=g)
     q.put((rank, x.cpu().numpy(), x2.cpu().numpy(), yb.cpu().numpy(), None if hb is None else hb.cpu().numpy(),
-           float(lb), None if rb is None else float(rb)))
+           float(lb), None if rb is None else float(rb), rec))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -98,45 +122,21 @@ def test_iso_uneven_shards_straddling_the_plane_count_rule(dev, need_rho, rule):
     _iso_sharded(dev, 256, need_rho, 0, nb=7, min_planes=rule)
 
 
-def _check_y_bar(yb, yb0):
-    """Sharded vs single-process y_bar.  The shards' batch norms are summed in another order than the single
-    process's, so ||s_k|| can differ in its last bit; where ||s_k|| is within that of tau the BT branch
-    1[||s_k|| > tau] flips, and the tau / ||s||^3 term moves y_bar of that PIXEL in every plane by far more than
-    rounding (test_gpu_adjoint_masked.py holds each sweep to 1e-5 against the oracle conditioned on its own
-    branches).  So: at most 0.1 % of the pixels may differ by more than 1e-3 max|y_bar| (such flips), and the
-    rest must agree to 1e-4 rel-L2.  A layout mix-up of the reducer's maps would corrupt every pixel."""
-    yb, yb0 = np.asarray(yb, np.float64), np.asarray(yb0, np.float64)
-    d = np.abs(yb - yb0).reshape(-1, *yb.shape[-2:]).max(axis=0)          # per pixel, over planes and channels
-    spots = d > 1e-3 * np.abs(yb0).max()
-    per_plane = [f"{_rel(yb[i], yb0[i]):.1e}" for i in range(yb.shape[0])]
-    assert spots.mean() <= 1e-3, f"{int(spots.sum())} pixels differ (per-plane rel-L2 {per_plane})"
-    keep = ~spots
-    rest = _rel(yb[..., keep], yb0[..., keep])
-    assert rest < 1e-4, f"y_bar away from {int(spots.sum())} flipped pixels: rel-L2 {rest:.2e} (per plane {per_plane})"
-
-
 def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
+    """The sharded solve against the fp64 oracle conditioned on ITS OWN trajectory's BT branches (the shards'
+    common batch norms), with the bounds of test_gpu_adjoint_masked.py (<= 1e-5, or the fp32 evaluation's error of
+    the same computation); the single-process solve the same way; and every BT branch in which the two runs
+    differ lies within rounding of tau in both (the sharded batch norm sums the planes in another order).  That
+    is the whole difference between them: the shards compute the exact adjoint of their own trajectory."""
+    import test_gpu_adjoint_masked as tm
+    import oracle_torch
     if resident:
         from admm_deconv import _lib
         assert _lib.query_paths(M, M, True, 7)[0] == "resident_iso"
     h, y, xbar = _inputs(M, nb)
     ht = torch.from_numpy(h).to(dev)
     x0 = admm_deconv.tvd_fft(torch.from_numpy(y).to(dev), LAM, RHO, ht, True, K).cpu().numpy()
-    _, yb0, hb0, lb0, rb0 = admm_deconv.tvd_fft_backward(torch.from_numpy(y).to(dev),
-                                                        torch.from_numpy(xbar).to(dev), LAM, RHO, ht, True, K,
-                                                        need_h=need_rho, need_rho=need_rho)
-    yb0, lb0 = yb0.cpu().numpy(), float(lb0)
-    # the spread of the scalar gradients under a reordered batch sum: the same single-process solve with the
-    # batch in other plane orders (mathematically identical: pixelnorm and every gradient sum over the planes)
-    spread = {"lam": 0.0, "rho": 0.0, "h": 0.0}
-    for order in (np.arange(nb)[::-1], np.r_[np.arange(0, nb, 2), np.arange(1, nb, 2)]):
-        _, _, hbp, lbp, rbp = admm_deconv.tvd_fft_backward(
-            torch.from_numpy(np.ascontiguousarray(y[order])).to(dev), torch.from_numpy(np.ascontiguousarray(xbar[order])).to(dev),
-            LAM, RHO, ht, True, K, need_h=need_rho, need_rho=need_rho)
-        spread["lam"] = max(spread["lam"], abs(float(lbp) - lb0))
-        if need_rho:
-            spread["rho"] = max(spread["rho"], abs(float(rbp) - float(rb0)))
-            spread["h"] = max(spread["h"], float(np.linalg.norm(hbp.cpu().numpy() - hb0.cpu().numpy())))
+    single = _record_and_replay(y, xbar, h, need_rho, dev)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -151,15 +151,28 @@ def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
     x = np.concatenate([r[1] for r in res])
     assert _rel(x, x0) < 1e-5
     assert _rel(np.concatenate([r[2] for r in res]), x0) < 1e-5
-    _check_y_bar(np.concatenate([r[3] for r in res]), yb0)
-    # scalar gradients: the shards' contributions add up to the whole batch's within 1e-3, widened by twice the
-    # reordered-batch spread (a BT branch flip moves them as it moves y_bar above; the sharded and the
-    # single-process sums are two orderings, each within that spread of the others)
-    assert abs(sum(r[5] for r in res) - lb0) <= 1e-3 * abs(lb0) + 2 * spread["lam"], (sum(r[5] for r in res), lb0, spread)
-    if need_rho:
-        hb0n = hb0.cpu().numpy()
-        dh = float(np.linalg.norm(sum(r[4] for r in res) - hb0n))
-        assert dh <= 1e-3 * float(np.linalg.norm(hb0n)) + 2 * spread["h"], (dh, spread)
-        assert abs(sum(r[6] for r in res) - float(rb0)) <= 1e-3 * abs(float(rb0)) + 2 * spread["rho"], spread
-    else:
-        assert rb0 is None and all(r[6] is None for r in res)
+    # the recorded sharded solve: both ranks hold the same batch norms (the reducer's all-reduced maps)
+    recs = [r[7] for r in res]
+    assert np.array_equal(recs[0][1], recs[1][1])
+    xs = np.concatenate([r[0] for r in recs])
+    ybs = np.concatenate([r[2] for r in recs])
+    hbs = None if recs[0][3] is None else sum(r[3] for r in recs)   # shard contributions add up
+    lbs = sum(r[4] for r in recs)
+    rbs = None if recs[0][5] is None else sum(r[5] for r in recs)
+    tau = np.float32(np.float32(LAM) / np.float32(RHO))
+    masks = oracle_torch.masks_from_trajectory(None, LAM, RHO, True, recs[0][1])
+    frac = tm.assert_prox_active(tm.mask_fraction(masks), f"sharded-{M}", False)
+    cid = f"sharded-iso-{M}-{nb}planes-{'rho' if need_rho else 'sweep'}"
+    err, ref32 = tm.compare_to_oracle(cid, y, xbar, h, LAM, RHO, K, True, masks, frac, xs, ybs, hbs, lbs, rbs)
+    tm.check(cid, err, ref32)
+    # the single-process recording, the same way
+    masks1 = oracle_torch.masks_from_trajectory(None, LAM, RHO, True, single[1])
+    err1, ref1 = tm.compare_to_oracle(cid + "-single", y, xbar, h, LAM, RHO, K, True, masks1, tm.mask_fraction(masks1),
+                                      *single[:1], *single[2:])
+    tm.check(cid + "-single", err1, ref1)
+    # where the two runs' BT branches differ, both norms are within rounding of tau
+    n1, ns = np.asarray(single[1], np.float64), np.asarray(recs[0][1], np.float64)
+    flip = (n1 > tau) != (ns > tau)
+    if flip.any():
+        dist_tau = np.maximum(np.abs(n1[flip] - tau), np.abs(ns[flip] - tau)) / tau
+        assert dist_tau.max() <= 1e-4, f"{int(flip.sum())} branch flips, up to {dist_tau.max():.2e} of tau away"

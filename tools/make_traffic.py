@@ -1,6 +1,8 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes per kernel class.
 
-usage: python tools/make_traffic.py CONFIG OUT.json gpurun_out/prof_TAG/pmc_fetch gpurun_out/prof_TAG/pmc_write [pmc_sq]
+usage: python tools/make_traffic.py CONFIG PLANES OUT.json gpurun_out/prof_TAG/pmc_fetch gpurun_out/prof_TAG/pmc_write [pmc_sq]
+
+PLANES = the plane count of the profiled launches (bench.py reports the figures only for launches of that size).
 
 hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024   (FETCH_SIZE reads half the bytes of
 a wide coalesced stream on gfx950 -- MI355X_MICROARCH.md, HBM section; WRITE_SIZE is exact for 16-B
@@ -39,8 +41,8 @@ def klass(name):
 
 
 def main():
-    cfg, out, fdir, wdir = sys.argv[1:5]
-    sq = load([sys.argv[5]]) if len(sys.argv) > 5 else {}
+    cfg, planes, out, fdir, wdir = sys.argv[1:6]
+    sq = load([sys.argv[6]]) if len(sys.argv) > 6 else {}
     f = load([fdir])
     w = load([wdir])
     res = json.load(open(out)) if os.path.exists(out) else {}
@@ -53,7 +55,8 @@ def main():
         ws = sum(w[name]["WRITE_SIZE"]) / len(w[name]["WRITE_SIZE"])
         ent[c] = {"kernel": name, "fetch_size_kib": fs, "write_size_kib": ws,
                   "hbm_bytes_per_launch": int(2 * fs * 1024 + ws * 1024),
-                  "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 correction); includes Infinity-Cache hits"}
+                  "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 correction); includes Infinity-Cache hits",
+                  "planes": int(planes)}
         if name in sq and "SQ_INSTS_VALU" in sq[name]:
             avg = lambda k: sum(sq[name][k]) / len(sq[name][k])
             # wave-level instruction counts per launch (SQ counters sum over the whole chip)
