@@ -1,11 +1,10 @@
 #!/bin/bash
-# c4 profiles (round 5): rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE / SQ passes of the 2-pass path and of
-# the persistent team512 launch (ADMM_EXP_TEAM512=1).  usage: tools/prof_c4.sh TAG
+# c4 profiles: rocprofv3 kernel stats + FETCH_SIZE / WRITE_SIZE / SQ passes of the 2-pass path (round 5 also profiled
+# the persistent team512 launch, now tools/variants/team512_line512.patch).  usage: tools/prof_c4.sh TAG
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
 TAG=${1:-c4}
-for v in 2pass team; do
-  if [ $v = team ]; then export ADMM_EXP_TEAM512=1; else unset ADMM_EXP_TEAM512; fi
+for v in 2pass; do
   OUT=gpurun_out/prof_${TAG}_$v; mkdir -p $OUT
   B="python bench.py --config c4 --no-cpu-baseline"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- $B --steps 3 --warmup 1 > $OUT/stats.log 2>&1 || exit $?

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 import admm_deconv  # noqa: E402
 from admm_deconv import _lib, synth  # noqa: E402
 
-# NAME=VALUE arguments are library options (admm_set_option), e.g. PLANE_STAGGER=3500
+# NAME=VALUE arguments are library options (admm_set_option), e.g. RESIDENT=2
 for _a in [a for a in sys.argv[1:] if "=" in a]:
     _lib.set_option(_a.split("=")[0].upper(), int(_a.split("=")[1]))
     sys.argv.remove(_a)
