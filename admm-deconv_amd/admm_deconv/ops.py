@@ -71,15 +71,27 @@ def _make_reducer(workspace, group):
             base = workspace._buf.data_ptr()
             off = int(buf) - base
             view = workspace._buf[off: off + 4 * int(count)].view(torch.float32)
-            on_dev = (torch.cuda.stream(torch.cuda.ExternalStream(int(stream or 0), device=view.device))
-                      if view.is_cuda else contextlib.nullcontext())
-            with on_dev:
+            ctx, lib_stream = contextlib.nullcontext(), None
+            if view.is_cuda:
+                # the stream the library enqueued the map on: handle 0 is torch's own default stream object (an
+                # ExternalStream wrapped around handle 0 did not order torch's copies after the library's kernels:
+                # a second sharded call read the map early, tests/test_gpu_dist_iso.py, round 6)
+                h = int(stream or 0)
+                cur = torch.cuda.current_stream(view.device)
+                lib_stream = (cur if cur.cuda_stream == h else torch.cuda.default_stream(view.device) if h == 0
+                              else torch.cuda.ExternalStream(h, device=view.device))
+                ctx = torch.cuda.stream(lib_stream)
+            with ctx:
                 if dist.get_backend(group) == "gloo":
+                    # host round trip (test infrastructure: gloo carries CPU tensors); the library launches its next
+                    # kernel as soon as this returns, so the copy back must have landed by then
                     host = view.cpu()
                     dist.all_reduce(host, group=group)
                     view.copy_(host)
+                    if lib_stream is not None:
+                        lib_stream.synchronize()
                 else:
-                    dist.all_reduce(view, group=group)
+                    dist.all_reduce(view, group=group)   # enqueued behind the library's work on its stream
             return 0
         except BaseException as e:   # an exception must not unwind through the C frames
             import sys

@@ -164,15 +164,24 @@ def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
     frac = tm.assert_prox_active(tm.mask_fraction(masks), f"sharded-{M}", False)
     cid = f"sharded-iso-{M}-{nb}planes-{'rho' if need_rho else 'sweep'}"
     err, ref32 = tm.compare_to_oracle(cid, y, xbar, h, LAM, RHO, K, True, masks, frac, xs, ybs, hbs, lbs, rbs)
-    tm.check(cid, err, ref32)
     # the single-process recording, the same way
     masks1 = oracle_torch.masks_from_trajectory(None, LAM, RHO, True, single[1])
     err1, ref1 = tm.compare_to_oracle(cid + "-single", y, xbar, h, LAM, RHO, K, True, masks1, tm.mask_fraction(masks1),
                                       *single[:1], *single[2:])
-    tm.check(cid + "-single", err1, ref1)
-    # where the two runs' BT branches differ, both norms are within rounding of tau
     n1, ns = np.asarray(single[1], np.float64), np.asarray(recs[0][1], np.float64)
     flip = (n1 > tau) != (ns > tau)
+    diag = (f"flips {int(flip.sum())}, |nrm_single - nrm_sharded| max {np.abs(n1 - ns).max():.3e} "
+            f"(rel {np.abs(n1 - ns).max() / np.abs(n1).max():.2e}); single vs its oracle {err1}; "
+            f"sharded y_bar vs single {_rel(ybs, single[2]):.3e}, x {_rel(xs, single[0]):.3e}; combined-call sharded "
+            f"y_bar vs single {_rel(np.concatenate([r[3] for r in res]), single[2]):.3e}, per rank rec vs comb "
+            f"{[_rel(r[7][2], r[3]) for r in res]}")
+    print(cid, diag, flush=True)
+    tm.check(cid + "-single", err1, ref1)
+    try:
+        tm.check(cid, err, ref32)
+    except AssertionError as e:
+        raise AssertionError(f"{e}; {diag}") from None
+    # where the two runs' BT branches differ, both norms are within rounding of tau
     if flip.any():
         dist_tau = np.maximum(np.abs(n1[flip] - tau), np.abs(ns[flip] - tau)) / tau
         assert dist_tau.max() <= 1e-4, f"{int(flip.sum())} branch flips, up to {dist_tau.max():.2e} of tau away"
