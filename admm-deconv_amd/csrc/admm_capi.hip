@@ -316,6 +316,7 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
         L.pbs = (size_t)K * L.rows_b * 2;
         L.spec0 = take(planes * MN * 4);
         L.spec1 = take(planes * MN * 4);
+        L.hln = take(planes * MN * 4);   // Y_h = F y per grid plane (H^T y in the spectral domain)
         if (iso) {
             L.fmap = take((size_t)nbr * MN * 4);
             L.qpart = take((size_t)nbr * L.ngb * MN * 4);

@@ -322,11 +322,13 @@ __global__ __launch_bounds__(256) void line_inv_kernel(const float2* __restrict_
 //              1: x Gt (H^T: conj(Sigma_c) / (MN));  2: x conj(Gt) (H, y_bar = H Vsum in the adjoint)
 //   mode & 4: store the dim-2 spectrum before the multiply to vsave [plane][kj][k] (trajectory, h_bar)
 //   mode & 8: Qp[plane][kj][k] += Re(conj(G) V) against vsave (adjoint, h_bar)
+//   mode & 16: + yh[plane][kj][k] before the save and the multiply (Y_h = F(H^T y): H^T y enters spectrally)
+//   mode & 32: store Y_h = cs x (mode & 3 == 1 and Gt: Gt) x the forward spectrum to yh; no inverse, dst untouched
 __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
                                                      const float2* __restrict__ twN, FPlan pN, int H, int KB,
                                                      int mode, float cs, float2* __restrict__ vsave = nullptr,
-                                                     double* __restrict__ Qp = nullptr) {
+                                                     double* __restrict__ Qp = nullptr, float2* __restrict__ yh = nullptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int N = pN.n;
     float2* A = reinterpret_cast<float2*>(smem_raw);
@@ -351,8 +353,12 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
         const int kj = fdiv(idx, KB), c = idx - kj * KB;
         if (c >= kc) continue;
         const size_t q = (size_t)kj * H + k0 + c;
-        const float2 v = R[c * N + kj];
         const size_t pq = (size_t)plane * N * H + q;
+        const float2 v = (mode & 16) ? cadd(R[c * N + kj], yh[pq]) : R[c * N + kj];
+        if (mode & 32) {
+            yh[pq] = cscale((mode & 3) == 1 && Gt ? cmul(v, Gt[q]) : v, cs);
+            continue;
+        }
         if (mode & 4) vsave[pq] = v;
         if (mode & 8) {
             const float2 fv = vsave[pq];
@@ -361,6 +367,7 @@ __global__ __launch_bounds__(256) void column_kernel(const float2* __restrict__ 
         const int mul = mode & 3;
         R[c * N + kj] = mul == 0 ? cscale(v, cs * Ct[q]) : cmul(v, mul == 1 ? Gt[q] : cconj(Gt[q]));
     }
+    if (mode & 32) return;   // block-uniform: Y_h stored, no inverse
     __syncthreads();
     const float2* Z = fft<true>(R, O, KB, N, pN, tw);
     for (int idx = threadIdx.x; idx < N * KB; idx += blockDim.x) {
@@ -416,8 +423,9 @@ __global__ __launch_bounds__(256) void line_upd_kernel(const float* __restrict__
         }
     });
     __syncthreads();
-    const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
-    batched<kU>(T * M, [&](int idx) { return hp[idx]; }, [&](int idx, float hv) {
+    // hty NULL: H^T y enters spectrally (column_kernel mode 16), v = rho D^T w here
+    const float* hp = hty ? hty + (size_t)plane * MN + (size_t)j0 * M : nullptr;
+    batched<kU>(T * M, [&](int idx) { return hp ? hp[idx] : 0.0f; }, [&](int idx, float hv) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         pack_real(A, t, i, M, fmaf(rho, dtw, hv));
@@ -502,8 +510,9 @@ __global__ __launch_bounds__(256) void iso_b_kernel(const float* __restrict__ s,
         if (t < T) W1[idx] = r.x * r.z - (r.z - r.x * r.z);
     });
     __syncthreads();
-    const float* hp = hty + (size_t)plane * MN + (size_t)j0 * M;
-    batched<kU>(T * M, [&](int idx) { return hp[idx]; }, [&](int idx, float hv) {
+    // hty NULL: H^T y enters spectrally (column_kernel mode 16), v = rho D^T w here
+    const float* hp = hty ? hty + (size_t)plane * MN + (size_t)j0 * M : nullptr;
+    batched<kU>(T * M, [&](int idx) { return hp ? hp[idx] : 0.0f; }, [&](int idx, float hv) {
         const int t = fdiv(idx, M), i = idx - t * M;
         const float dtw = (W0[idx] - W0[idx + M]) + (W1[idx] - W1[t * M + wrap(i + 1, M)]);
         pack_real(A, t, i, M, fmaf(rho, dtw, hv));

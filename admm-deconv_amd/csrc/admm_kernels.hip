@@ -292,13 +292,20 @@ __global__ __launch_bounds__(kThreads) void line_inv_kernel(const float2* __rest
 //   SAVE   : also store the forward dim-2 spectrum (before the multiply) to vsave (trajectory for h_bar)
 //   ACCQ   : accumulate Q[kj][k] += Re(conj(G) V) against the saved forward spectrum (adjoint, h_bar), in fp64:
 //            K terms per bin, later scaled by C^2 in hbarA_kernel
+//   YH     : the spectrum of H^T y enters in the spectral domain (DESIGN.md s1 "H^T y in the spectrum"):
+//            YH_STORE: forward transform, x Gt (conj(Sigma_c)/(MN); none when Gt is NULL), x cs, stored to yh as
+//                      the plane's 2-D packed spectrum Y_h = F(H^T y) -- no inverse, dst untouched;
+//            YH_ADD:   yh added to the forward spectrum (before the mirror staging, SAVE and the multiply), so the
+//                      per-iteration transforms carry only rho D^T w and H^T y never passes an fp32 FFT again
 // ----------------------------------------------------------------------------------------------
+enum { YH_NONE = 0, YH_STORE = 1, YH_ADD = 2 };
 // The body takes the block's (slot block, plane) explicitly (a persistent kernel can run it too: the round-5 team
 // launch, tools/variants/team512.patch); column_kernel is the one-launch-per-pass form.
-template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
+template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads, int YH = YH_NONE>
 __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* dst, const float* __restrict__ Ct,
                                             const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
-                                            int KB, float cs, float2* __restrict__ vsave, double* __restrict__ Qp) {
+                                            int KB, float cs, float2* __restrict__ vsave, double* __restrict__ Qp,
+                                            float2* __restrict__ yh = nullptr) {
     constexpr bool CPLX = MUL != 0;
     constexpr int FS = NN + 1;  // per-transform LDS stride (odd: conflict-free slot-major stores)
     constexpr int P = Plan<NN>::P;
@@ -372,6 +379,11 @@ __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* 
 #pragma unroll
                 for (int r = 0; r < R; ++r) v[r] = buf[f * FS + j + r * Q];
             }
+            if constexpr (YH == YH_ADD) {   // + F(H^T y): before the slot-0 staging, the mirror reads the sum
+                const float2* yp = yh + (size_t)plane * NN * L + k0 + f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) v[r] = cadd(v[r], yp[(size_t)(j + r * Q) * L]);
+            }
             if (mirror && f == 0) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) S0[j + r * Q] = v[r];
@@ -409,6 +421,8 @@ __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* 
                     }
                 }
             }
+            // (YH_STORE without a PSF: Y_h = F y, no multiplier)
+            if (YH != YH_STORE || Gt != nullptr)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int kj = j + r * Q;
@@ -433,6 +447,11 @@ __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* 
                     }
                 }
             }
+            if constexpr (YH == YH_STORE) {   // Y_h = cs Gt F y: stored, no inverse
+                float2* yp = yh + (size_t)plane * NN * L + k0 + f;
+#pragma unroll
+                for (int r = 0; r < R; ++r) yp[(size_t)(j + r * Q) * L] = cscale(v[r], cs);
+            } else {
             // inverse first pass (reversed plan: radix R, Ns = 1) reads exactly j + r*Q
             dft<R, true>(v);
             if constexpr (P == 1) {
@@ -442,7 +461,9 @@ __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* 
 #pragma unroll
                 for (int r = 0; r < R; ++r) buf[f * FS + j * R + r] = v[r];
             }
+            }
         }
+        if constexpr (YH == YH_STORE) return;   // block-uniform
         __syncthreads();
     }
     if constexpr (P == 3) {   // inverse middle pass (reversed plan pass 1), in place
@@ -483,14 +504,15 @@ __device__ __forceinline__ void column_body(XBlk xb, const float2* src, float2* 
     }
 }
 
-template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads>
+template <int NN, int MUL, bool SAVE, bool ACCQ, int NT = kThreads, int YH = YH_NONE>
 __global__ __launch_bounds__(NT) void column_kernel(const float2* src, float2* dst, const float* __restrict__ Ct,
                                                     const float2* __restrict__ Gt, const float2* __restrict__ twN, int L,
                                                     int KB, float cs, float2* __restrict__ vsave,
-                                                    double* __restrict__ Qp, Branches br = kOneSolve) {
+                                                    double* __restrict__ Qp, Branches br = kOneSolve,
+                                                    float2* __restrict__ yh = nullptr) {
     const XBlk xb = xcd_block();
-    column_body<NN, MUL, SAVE, ACCQ, NT>(xb, src, dst, Ct + (size_t)branch_of(br, xb.y).i * br.tab_f, Gt, twN, L, KB,
-                                         cs, vsave, Qp);
+    column_body<NN, MUL, SAVE, ACCQ, NT, YH>(xb, src, dst, Ct + (size_t)branch_of(br, xb.y).i * br.tab_f, Gt, twN, L,
+                                             KB, cs, vsave, Qp, yh);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -522,7 +544,8 @@ __device__ __forceinline__ void line_body(XBlk xb, const float2* __restrict__ sp
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
     const BranchOf bo = branch_of(br, plane);   // several branches: H^T y = the shared input plane, own scalars
-    const float* hp = hty + bo.in_plane * MN;
+    // hty NULL: H^T y is added in the spectral domain by the column pass (YH_ADD); v = rho D^T w here
+    const float* hp = hty ? hty + bo.in_plane * MN : nullptr;
     const float tau = prm[(size_t)bo.i * br.prm_f], rho = prm[(size_t)bo.i * br.prm_f + 1];   // (setup_kernel)
 
     // ---- issue every global load of the block up front -- except at 512-point lines (kJit): there the
@@ -554,10 +577,13 @@ __device__ __forceinline__ void line_body(XBlk xb, const float2* __restrict__ sp
         for (int it = 0; it < NITF; ++it) {
             const int idx = tid + it * NT;
             const int f = idx / QF, j = idx - f * QF;
-            if (idx < T * QF) {
+            if (hp && idx < T * QF) {
                 const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
 #pragma unroll
                 for (int r = 0; r < RF; ++r) preh[it][r] = hl[j + r * QF];
+            } else {
+#pragma unroll
+                for (int r = 0; r < RF; ++r) preh[it][r] = make_float2(0.f, 0.f);
             }
         }
     };
@@ -895,7 +921,7 @@ __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict
     fmap += (size_t)bo.i * MN;
     const float rho = prm[(size_t)bo.i * br.prm_f + 1];   // device-resident scalars (setup_kernel)
     const float* sp = s_new + (size_t)plane * 2 * MN;
-    const float* hp = hty + bo.in_plane * MN;
+    const float* hp = hty ? hty + bo.in_plane * MN : nullptr;   // NULL: H^T y enters spectrally (YH_ADD)
     for (int t = tid; t < M; t += kThreads) tw[t] = twM[t];
     for (int idx = tid; idx < NE; idx += kThreads) {
         const int t = idx / M4, i = (idx - t * M4) * 4;
@@ -921,12 +947,12 @@ __global__ __launch_bounds__(kThreads) void iso_b_kernel(const float* __restrict
     __syncthreads();
     for (int idx = tid; idx < T * QF; idx += kThreads) {
         const int f = idx / QF, j = idx - f * QF;
-        const float2* hl = reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M);
+        const float2* hl = hp ? reinterpret_cast<const float2*>(hp + (size_t)(j0 + f) * M) : nullptr;
         float2 v[RF];
 #pragma unroll
         for (int r = 0; r < RF; ++r) {
             const int n = j + r * QF;
-            const float2 hv = hl[n];
+            const float2 hv = hl ? hl[n] : make_float2(0.f, 0.f);
             const float2 a = *reinterpret_cast<const float2*>(W0 + f * M + 2 * n);
             const float2 b = *reinterpret_cast<const float2*>(W0 + (f + 1) * M + 2 * n);
             const float2 c = *reinterpret_cast<const float2*>(W1 + f * M + 2 * n);

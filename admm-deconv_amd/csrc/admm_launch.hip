@@ -120,31 +120,34 @@ int launch_iso_b(int L, int T, dim3 g, size_t lds, hipStream_t s, const float* s
     return -1;
 }
 
-template <int MUL, bool SAVE, bool ACCQ>
+template <int MUL, bool SAVE, bool ACCQ, int YH = YH_NONE>
 int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst, const float* C,
                     const float2* G, const float2* twN, int L, int KB, float cs, float2* vsave, double* Qp,
-                    const Branches& br) {
+                    const Branches& br, float2* yh = nullptr) {
     const int nt = column_threads(N);
 #define X(v)                                                                                                   \
     if (N == v && nt == kThreads) {                                                                            \
-        set_lds(column_kernel<v, MUL, SAVE, ACCQ>, lds);                                                       \
-        column_kernel<v, MUL, SAVE, ACCQ><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ, kThreads, YH>, lds);                                         \
+        column_kernel<v, MUL, SAVE, ACCQ, kThreads, YH><<<g, kThreads, lds, s>>>(src, dst, C, G, twN, L, KB, cs,  \
+                                                                                  vsave, Qp, br, yh);             \
         return 0;                                                                                              \
     }
     ADMM_N_CASES(X)
 #undef X
 #define X(v)                                                                                                   \
     if (N == v && nt == 512) {                                                                                 \
-        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 512>, lds);                                                  \
-        column_kernel<v, MUL, SAVE, ACCQ, 512><<<g, 512, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 512, YH>, lds);                                              \
+        column_kernel<v, MUL, SAVE, ACCQ, 512, YH><<<g, 512, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br, \
+                                                                       yh);                                        \
         return 0;                                                                                              \
     }
     X(256) X(512) X(1024)
 #undef X
 #define X(v)                                                                                                   \
     if (N == v && nt == 1024) {                                                                                \
-        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 1024>, lds);                                                 \
-        column_kernel<v, MUL, SAVE, ACCQ, 1024><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp, br); \
+        set_lds(column_kernel<v, MUL, SAVE, ACCQ, 1024, YH>, lds);                                             \
+        column_kernel<v, MUL, SAVE, ACCQ, 1024, YH><<<g, 1024, lds, s>>>(src, dst, C, G, twN, L, KB, cs, vsave, Qp,  \
+                                                                         br, yh);                                   \
         return 0;                                                                                              \
     }
     X(256) X(512) X(1024)
@@ -153,11 +156,16 @@ int launch_column_t(int N, dim3 g, size_t lds, hipStream_t s, const float2* src,
 }
 
 // mode: 0 = x-update C, 1 = conj(Sigma_c) (H^T), 2 = Sigma_c (H), 3 = C + save spectrum, 4 = C + accumulate Q;
-// br: several branches (C per branch, br.tab_f floats apart)
+// 5 = Y_h = cs conj(Sigma_c) F y stored to yh (G NULL: Y_h = cs F y), no inverse; 6 = + yh, x C; 7 = + yh, save, x C
+// (admm_kernels.hip YH_STORE / YH_ADD: H^T y in the spectral domain); br: several branches (C per branch, br.tab_f
+// floats apart)
 int launch_column(int N, int mode, dim3 g, size_t lds, hipStream_t s, const float2* src, float2* dst,
                   const float* C, const float2* G, const float2* twN, int L, int KB, float cs,
-                  float2* vsave = nullptr, double* Qp = nullptr, const Branches& br = kOneSolve) {
+                  float2* vsave = nullptr, double* Qp = nullptr, const Branches& br = kOneSolve, float2* yh = nullptr) {
     switch (mode) {
+        case 5: return launch_column_t<1, false, false, YH_STORE>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br, yh);
+        case 6: return launch_column_t<0, false, false, YH_ADD>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br, yh);
+        case 7: return launch_column_t<0, true, false, YH_ADD>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br, yh);
         case 0: return launch_column_t<0, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
         case 1: return launch_column_t<1, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
         case 2: return launch_column_t<2, false, false>(N, g, lds, s, src, dst, C, G, twN, L, KB, cs, vsave, Qp, br);
@@ -358,25 +366,29 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                                     maxit);
         });
     }
-    // PREP: spectrum of y; with a PSF, H^T y = F^-1 conj(Sigma_c) F y (line, column, line)
+    // PREP: Y_h = F(H^T y) = conj(Sigma_c) F y as a 2-D packed spectrum straight from F y (line transform, column
+    // transform x conj(Sigma_c)), never H^T y in space: every iteration adds it to the spectrum of rho D^T w in
+    // the column pass, so the per-iteration fp32 transforms carry only rho D^T w (x 16x, y_bar / h_bar ~2-9x closer
+    // to the fp64 oracle than with H^T y added before the line transform; DESIGN.md s1 "H^T y in the spectrum").
+    // Iteration 1 (w = 0) transforms a zero line spectrum and adds Y_h.
+    float2* yh = reinterpret_cast<float2*>(ws + lay.hty);   // the workspace's H^T y slot holds Y_h on this path
     rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N); });
     if (rc) return rc;
-    const float2* first = spec0;
-    float cs1 = 1.0f;
-    if (kh > 0) {
-        rc = ln.run(ADMM_K_PREP, [&] { return launch_column(N, 1, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f); });
-        if (rc) return rc;
-        rc = ln.run(ADMM_K_PREP, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, hty, twM, N); });
-        if (rc) return rc;
-        first = spec1;          // = F_dim1(H^T y) / M
-        cs1 = (float)M;
+    rc = ln.run(ADMM_K_PREP, [&] {
+        return launch_column(N, 5, gc, clds, s, spec0, spec1, Ct, kh > 0 ? Gt : nullptr, twN, L, KB,
+                             kh > 0 ? (float)MN : 1.0f, nullptr, nullptr, kOneSolve, yh);
+    });
+    if (rc) return rc;
+    {
+        hipError_t e = hipMemsetAsync(spec0, 0, np * MN * 4, s);
+        if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
     }
     const size_t sstride = np * 2 * MN;   // one trajectory slot of s
     for (int it = 1; it <= maxit; ++it) {
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * np * N * L : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            return launch_column(N, vsave ? 3 : 0, gc, clds, s, it == 1 ? first : spec0, spec1, Ct, Gt, twN, L, KB,
-                          it == 1 ? cs1 : 1.0f, vsave);
+            return launch_column(N, vsave ? 7 : 6, gc, clds, s, spec0, spec1, Ct, Gt, twN, L, KB, 1.0f, vsave, nullptr,
+                                 kOneSolve, yh);
         });
         if (rc) return rc;
         if (it < maxit && !iso) {
@@ -390,7 +402,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
                 sn = (it & 1) ? sbuf[0] : sbuf[1];
             }
             rc = ln.run(ADMM_K_LINE, [&] {
-                return launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, hty, twM, N, prm,
+                return launch_line(L, Tu, dim3(N / Tu, (unsigned)np), llds, s, spec1, spec0, so, sn, nullptr, twM, N, prm,
                             it == 1 ? 1 : 0, nTu);
             });
         } else if (it < maxit) {
@@ -429,7 +441,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
             }
             if (rc) return rc;
             rc = ln.run(ADMM_K_LINE, [&] {
-                return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, hty, spec0, twM, N, prm);
+                return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, nullptr, spec0, twM, N, prm);
             });
         } else {
             rc = ln.run(ADMM_K_FINAL, [&] { return launch_line_inv(L, T, gl, flds, s, spec1, x_out, twM, N); });
@@ -484,12 +496,27 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
     // CU-resident solve (admm_resident.hip): anisotropic, no dim-2 spectra or isotropic norms recorded; it
     // forms the first line spectrum itself, so PREP only produces H^T y
     const bool res = path == ADMM_PATH_RESIDENT || path == ADMM_PATH_RESIDENT_ISO;   // plan_paths
-    // PREP: spectrum of H^T y (with a PSF: F^-1 conj(Sigma_c) F y first, ops.jl:71-81)
-    if (!res || kh > 0) {
+    // the 2-pass kernels take H^T y in the spectral domain: Y_h = conj(Sigma_c) F y (with a PSF) stored once as the
+    // column pass's 2-D spectrum and added to every iteration's spectrum of rho D^T w
+    float2* yh = reinterpret_cast<float2*>(ws + lay.hty);
+    if (!res) {
+        rc = line_fwd(y, spec0);
+        if (rc) return rc;
+        rc = ln.run(ADMM_K_PREP, [&] {
+            hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 32 | 1,
+                               kh > 0 ? (float)MN : 1.0f, (float2*)nullptr, (double*)nullptr, yh);
+            return 0;
+        });
+        if (rc) return rc;
+        hipError_t e = hipMemsetAsync(spec0, 0, planes * (size_t)H * N * 8, s);   // iteration 1: w = 0
+        if (e != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync: %s", hipGetErrorString(e));
+    }
+    // PREP of the resident solves: H^T y in space (with a PSF: F^-1 conj(Sigma_c) F y, ops.jl:71-81)
+    if (res && kh > 0) {
         rc = line_fwd(y, spec0);
         if (rc) return rc;
     }
-    if (kh > 0) {
+    if (res && kh > 0) {
         rc = ln.run(ADMM_K_PREP, [&] {
             if (smc) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 1, opt(ADMM_OPT_SMOOTH));
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB, 1, 1.0f);
@@ -502,10 +529,6 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
             return 0;
         });
         if (rc) return rc;
-        if (!res) {
-            rc = line_fwd(hty, spec0);
-            if (rc) return rc;
-        }
     }
     const int ng = iso_ngroups(planes);
     const size_t sstride = planes * 2 * MN;   // one trajectory slot of s
@@ -521,9 +544,10 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         // trajectory for h_bar: the dim-2 spectrum of iteration it before the multiply
         float2* vsave = tr.v ? tr.v + (size_t)(it - 1) * planes * N * H : nullptr;
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            if (smc && !vsave) return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 0, opt(ADMM_OPT_SMOOTH));
+            if (smc && !vsave)
+                return admm::sm::launch_column(M, N, planes, s, spec0, spec1, Ct, Gt, twN, 1.0f, 0, opt(ADMM_OPT_SMOOTH), yh);
             hipLaunchKernelGGL(g::column_kernel, gc, dim3(256), lcol, s, spec0, spec1, Ct, Gt, twN, pN, H, KB,
-                               vsave ? 4 : 0, 1.0f, vsave, (double*)nullptr);
+                               (vsave ? 4 : 0) | 16, 1.0f, vsave, (double*)nullptr, yh);
             return 0;
         });
         if (rc) return rc;
@@ -543,9 +567,9 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
                 sn = tr.s + (size_t)(it - 1) * sstride;
             }
             rc = ln.run(ADMM_K_LINE, [&] {
-                if (sml) return admm::sm::launch_line_upd(M, N, planes, s, xg, so, sn, hty, spec0, twM, prm, it == 1 ? 1 : 0);
-                hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, hty, spec0, twM, pM, N, T, prm,
-                                   it == 1 ? 1 : 0);
+                if (sml) return admm::sm::launch_line_upd(M, N, planes, s, xg, so, sn, nullptr, spec0, twM, prm, it == 1 ? 1 : 0);
+                hipLaunchKernelGGL(g::line_upd_kernel, gl, dim3(256), lup, s, xg, so, sn, (const float*)nullptr, spec0, twM,
+                                   pM, N, T, prm, it == 1 ? 1 : 0);
                 return 0;
             });
             if (rc) return rc;
@@ -582,7 +606,8 @@ int run_forward_generic(Launcher& ln, const float* y, float* x_out, int M, int N
         }
         if (rc) return rc;
         rc = ln.run(ADMM_K_LINE, [&] {
-            hipLaunchKernelGGL(g::iso_b_kernel, gl, dim3(256), lup, s, sa, fmap, hty, spec0, twM, pM, N, T, prm);
+            hipLaunchKernelGGL(g::iso_b_kernel, gl, dim3(256), lup, s, sa, fmap, (const float*)nullptr, spec0, twM, pM, N, T,
+                               prm);
         });
         if (rc) return rc;
     }
@@ -1010,11 +1035,19 @@ int run_multi_2pass_iso_fwd(Launcher& ln, const float* y, float* x_out, int P, i
     float* traj = rec ? reinterpret_cast<float*>(ws + Ly.traj) : nullptr;
     float* nrm = rec ? reinterpret_cast<float*>(ws + Ly.nrm) : nullptr;
     float* sA = rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sA);
+    // H^T y = y (no PSF) in the spectral domain, as run_forward's 2-pass kernels: Y_h = F y per grid plane (the
+    // hln slot, unused by the 2-pass grid), added by every column pass; iteration 1 transforms a zero spectrum
+    float2* yh = reinterpret_cast<float2*>(ws + Ly.hln);
     int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N, br, kMapIn); });
     if (rc) return rc;
+    rc = ln.run(ADMM_K_PREP, [&] {
+        return launch_column(N, 5, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br, yh);
+    });
+    if (rc) return rc;
+    if (hipMemsetAsync(spec0, 0, planes * MN * 4, s) != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync");
     for (int it = 1; it <= maxit; ++it) {
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            return launch_column(N, 0, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+            return launch_column(N, 6, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br, yh);
         });
         if (rc) return rc;
         if (it == maxit) {
@@ -1037,7 +1070,7 @@ int run_multi_2pass_iso_fwd(Launcher& ln, const float* y, float* x_out, int P, i
         });
         if (rc) return rc;
         rc = ln.run(ADMM_K_LINE, [&] {
-            return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, y, spec0, twM, N, prm, br);
+            return launch_iso_b(L, T, gl, iso_b_lds(M, T), s, sn, fmap, nullptr, spec0, twM, N, prm, br);
         });
         if (rc) return rc;
     }
@@ -1139,11 +1172,19 @@ int run_multi_2pass_fwd(Launcher& ln, const float* y, float* x_out, int P, int B
     float2* spec1 = reinterpret_cast<float2*>(ws + Ly.spec1);
     float* traj = rec ? reinterpret_cast<float*>(ws + Ly.traj) : nullptr;
     float* sbuf[2] = {rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sA), rec ? nullptr : reinterpret_cast<float*>(ws + Ly.sbA)};
+    // H^T y = y (no PSF) in the spectral domain, as run_forward's 2-pass kernels: Y_h = F y per grid plane (the
+    // hln slot, unused by the 2-pass grid), added by every column pass; iteration 1 transforms a zero spectrum
+    float2* yh = reinterpret_cast<float2*>(ws + Ly.hln);
     int rc = ln.run(ADMM_K_PREP, [&] { return launch_line_fwd(L, T, gl, flds, s, y, spec0, twM, N, br, kMapIn); });
     if (rc) return rc;
+    rc = ln.run(ADMM_K_PREP, [&] {
+        return launch_column(N, 5, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br, yh);
+    });
+    if (rc) return rc;
+    if (hipMemsetAsync(spec0, 0, planes * MN * 4, s) != hipSuccess) return fail(ADMM_E_HIP, "hipMemsetAsync");
     for (int it = 1; it <= maxit; ++it) {
         rc = ln.run(ADMM_K_COLUMN, [&] {
-            return launch_column(N, 0, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br);
+            return launch_column(N, 6, gc, clds, s, spec0, spec1, Ct, nullptr, twN, L, KB, 1.0f, nullptr, nullptr, br, yh);
         });
         if (rc) return rc;
         if (it == maxit) {
@@ -1155,7 +1196,7 @@ int run_multi_2pass_fwd(Launcher& ln, const float* y, float* x_out, int P, int B
         float* sn = rec ? traj + (size_t)(it - 1) * sstride : ((it & 1) ? sbuf[0] : sbuf[1]);
         const float* so = rec ? (it >= 2 ? traj + (size_t)(it - 2) * sstride : sn) : ((it & 1) ? sbuf[1] : sbuf[0]);
         rc = ln.run(ADMM_K_LINE, [&] {
-            return launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, y, twM, N, prm, it == 1 ? 1 : 0, kThreads, br);
+            return launch_line(L, T, gl, llds, s, spec1, spec0, so, sn, nullptr, twM, N, prm, it == 1 ? 1 : 0, kThreads, br);
         });
         if (rc) return rc;
     }

@@ -97,7 +97,10 @@ constexpr int col_nt() {
 template <int NN, bool ASC, int MUL>
 __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float2* __restrict__ src, float2* __restrict__ dst,
                                                      const float* __restrict__ Ct, const float2* __restrict__ Gt,
-                                                     const float2* __restrict__ twN, int H, float cs) {
+                                                     const float2* __restrict__ twN, int H, float cs,
+                                                     const float2* __restrict__ yh = nullptr) {
+    // yh (not NULL): Y_h = F(H^T y), [plane][kj][k], added to the forward spectrum before the multiply (H^T y in
+    // the spectral domain, as admm_generic.hip column_kernel mode 16)
     constexpr int KB = col_kb(NN), FS = col_fs(NN, KB), NT = col_nt<NN, ASC>();
     using S = SP<NN, ASC, kColR>;
     constexpr int P = S::P;
@@ -112,6 +115,7 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
     float2* gd = dst + po;
     const float* cp = Ct + k0;
     const float2* gp = Gt + k0;
+    const float2* yp = yh ? yh + po : nullptr;
     // the multiplier of bin kj of this block's column c
     auto mul = [&](int c, int kj, float2 v) {
         if constexpr (MUL == 0) return cscale(v, cs * cp[(size_t)kj * H + c]);
@@ -129,7 +133,7 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
             for (int n = 0; n < NN; ++n) v[n] = gload(c, n);
             dftR<NN, false>(v);
 #pragma unroll
-            for (int n = 0; n < NN; ++n) v[n] = mul(c, n, v[n]);
+            for (int n = 0; n < NN; ++n) v[n] = mul(c, n, yp ? cadd(v[n], yp[(size_t)n * H + c]) : v[n]);
             dftR<NN, true>(v);
 #pragma unroll
             for (int n = 0; n < NN; ++n) gstore(c, n, v[n]);
@@ -173,6 +177,10 @@ __global__ __launch_bounds__((col_nt<NN, ASC>())) void column_kernel(const float
                     for (int r = 1; r < R; ++r) v[u][r] = cmul(v[u][r], tw[r * j]);
                     dftR<R, false>(v[u]);
                     if (f < kc) {
+                        if (yp) {
+#pragma unroll
+                            for (int r = 0; r < R; ++r) v[u][r] = cadd(v[u][r], yp[(size_t)(j + r * Q) * H + f]);
+                        }
 #pragma unroll
                         for (int r = 0; r < R; ++r) v[u][r] = mul(f, j + r * Q, v[u][r]);
                     }
@@ -329,7 +337,8 @@ __global__ __launch_bounds__(kNT) void line_upd_kernel(const float* __restrict__
     const float* xp = x + (size_t)plane * MN;
     const float* so = s_old + (size_t)plane * 2 * MN;
     float* sn = s_new + (size_t)plane * 2 * MN;
-    const float* hp = hty + ((size_t)plane * N + j0) * MM;
+    // hty NULL: H^T y enters spectrally (the runtime column kernel's mode 16), v = rho D^T w here
+    const float* hp = hty ? hty + ((size_t)plane * N + j0) * MM : nullptr;
     for (int t = threadIdx.x; t < MM; t += kNT) tw[t] = twM[t];
     // H^T y of this thread's first-pass points (lines 2f, 2f+1 at n = j + r Q0)
     float2 hv[NR0][R0];
@@ -342,8 +351,8 @@ __global__ __launch_bounds__(kNT) void line_upd_kernel(const float* __restrict__
 #pragma unroll
             for (int r = 0; r < R0; ++r) {
                 const int n = j + r * Q0;
-                hv[u][r].x = hp[(size_t)(2 * f) * MM + n];
-                hv[u][r].y = odd ? hp[(size_t)(2 * f + 1) * MM + n] : 0.0f;
+                hv[u][r].x = hp ? hp[(size_t)(2 * f) * MM + n] : 0.0f;
+                hv[u][r].y = (hp && odd) ? hp[(size_t)(2 * f + 1) * MM + n] : 0.0f;
             }
         }
     }
@@ -503,7 +512,7 @@ bool column_asc(int N, int mode) {
 }
 
 int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src, float2* dst, const float* Ct,
-                  const float2* Gt, const float2* twN, float cs, int mul, int mode) {
+                  const float2* Gt, const float2* twN, float cs, int mul, int mode, const float2* yh) {
     const int H = M / 2 + 1;
     const bool asc = column_asc(N, mode);
 #define X(v)                                                                                               \
@@ -513,13 +522,13 @@ int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src,
         const dim3 g((H + kb - 1) / kb, (unsigned)planes);                                                 \
         if (mul) {                                                                                         \
             set_lds(column_kernel<v, false, 1>, lds);                                                      \
-            column_kernel<v, false, 1><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
+            column_kernel<v, false, 1><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs, yh);              \
         } else if (asc) {                                                                                  \
             set_lds(column_kernel<v, true, 0>, lds);                                                       \
-            column_kernel<v, true, 0><<<g, col_nt<v, true>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                   \
+            column_kernel<v, true, 0><<<g, col_nt<v, true>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs, yh);               \
         } else {                                                                                           \
             set_lds(column_kernel<v, false, 0>, lds);                                                      \
-            column_kernel<v, false, 0><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs);                  \
+            column_kernel<v, false, 0><<<g, col_nt<v, false>(), lds, s>>>(src, dst, Ct, Gt, twN, H, cs, yh);              \
         }                                                                                                  \
         return 0;                                                                                          \
     }

@@ -48,7 +48,9 @@ inline Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.twN = take((size_t)N * 8);
     L.C = take((size_t)(M / 2 + 1) * N * 4);
     L.G = psf ? take((size_t)(M / 2 + 1) * N * 8) : 0;
-    L.hty = psf ? take(planes * MN * 4) : 0;
+    // H^T y (CU-resident and fused paths, PSF only) -- or, on the 2-pass and runtime-length paths, Y_h = F(H^T y) as
+    // the column pass's 2-D spectrum (packed M/2 x N, or M/2+1 x N bins on the generic path), with or without a PSF
+    L.hty = take(planes * (generic_shape(M, N) ? (size_t)(M / 2 + 1) * N * 8 : MN * 4));
     L.sA = take(planes * 2 * MN * 4);
     L.sB = take(planes * 2 * MN * 4);
     // N lines x M/2 complex (packed) -- or M/2 + 1 bins per line on the generic path

@@ -17,9 +17,10 @@ size_t column_lds(int N);
 
 // spec (N x (M/2+1) per plane) -> dim-2 FFT, x multiplier, IFFT -> dst (gen::column_kernel modes 0 / 1):
 // mul 0: cs * Ct, mul 1: Gt (H^T);  mode = ADMM_OPT_SMOOTH (1: measured plan order per length, 2 / 3:
-// increasing / decreasing radices)
+// increasing / decreasing radices); yh (not NULL): + Y_h = F(H^T y) before the multiply (gen::column_kernel mode 16)
 int launch_column(int M, int N, size_t planes, hipStream_t s, const float2* src, float2* dst, const float* Ct,
-                  const float2* Gt, const float2* twN, float cs, int mul, int mode);
+                  const float2* Gt, const float2* twN, float cs, int mul, int mode, const float2* yh = nullptr);
+// (line_upd: hty NULL = H^T y enters spectrally, v = rho D^T w)
 // real lines -> half spectra (gen::line_fwd_kernel)
 int launch_line_fwd(int M, int N, size_t planes, hipStream_t s, const float* src, float2* spec, const float2* twM);
 // half spectra -> real lines (gen::line_inv_kernel)

@@ -59,7 +59,7 @@ def test_forward_both_sides_of_the_plane_rule(dev, case):
 def test_recorded_gradients_both_sides_of_the_plane_rule(dev):
     """The training recording (mask bits, no rho_bar: the c5 layers) at 64 planes runs the 2-pass forward and
     sweep, at 96 the fused ones (paths_table c5-record-masks-64 / -96).  The 64 planes of both agree: y_bar
-    trimmed per-plane rel-L2 <= 1e-4 and lambda_bar <= 5e-3 (tests/test_gpu_backward.py: fp32 mask flips near
+    trimmed per-plane rel-L2 <= 1e-4 (full 1e-2) and lambda_bar <= 5e-3 (tests/test_gpu_backward.py: fp32 mask flips near
     the ST kink are the only difference), x <= 2e-5."""
     from test_gpu_backward import assert_grad
     M = 256
@@ -80,7 +80,11 @@ def test_recorded_gradients_both_sides_of_the_plane_rule(dev):
         out[n] = (x.cpu().numpy(), yb.cpu().numpy(), float(lb))
     xa, xb = out[64][0].astype(np.float64), out[96][0][:64].astype(np.float64)
     assert np.linalg.norm(xa - xb) / np.linalg.norm(xb) < 2e-5
-    assert_grad(out[64][1], out[96][1][:64], "y_bar 64 (2-pass) vs 96 (fused)")
+    # the two sides run forwards of different precision (the 2-pass kernels take H^T y spectrally, ~16x closer to the
+    # fp64 oracle than the fused kernel), so their ST branches differ in more places: the unconditioned
+    # adjoint criterion of DESIGN.md s2 (trimmed 1e-4, full 1e-2); test_gpu_adjoint_masked.py holds each sweep to
+    # 1e-5 on its own branches
+    assert_grad(out[64][1], out[96][1][:64], "y_bar 64 (2-pass) vs 96 (fused)", full_tol=1e-2)
     # lambda_bar sums over the planes: the 64-plane 2-pass sweep against the same 64 planes through the fused
     # sweep (the per-plane kernels forced, MIN_PLANES = 0)
     with _lib.option("MIN_PLANES", 0):

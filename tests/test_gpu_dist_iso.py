@@ -176,11 +176,19 @@ def _iso_sharded(dev, M, need_rho, resident, nb=B, min_planes=0):
             f"y_bar vs single {_rel(np.concatenate([r[3] for r in res]), single[2]):.3e}, per rank rec vs comb "
             f"{[_rel(r[7][2], r[3]) for r in res]}")
     print(cid, diag, flush=True)
+    # the unsharded solve against its own branches: test_gpu_adjoint_masked.py's bound (<= 1e-5, or the fp32
+    # evaluation's error of the same computation)
     tm.check(cid + "-single", err1, ref1)
-    try:
-        tm.check(cid, err, ref32)
-    except AssertionError as e:
-        raise AssertionError(f"{e}; {diag}") from None
+    # the sharded solve against its own branches: the same bound, or -- sharding must add no error of its own --
+    # the unsharded solve's error on the same computation (+5 % for the shards' reordered fp32 batch sums).  The
+    # 256^2 sweep cases run the fused isotropic kernels, whose H^T y still passes every iteration's fp32 transforms
+    # and sits at the fp32 level; the 2-pass paths are an order of magnitude below it.
+    for k in err:
+        bound = max(tm.TOL, ref32.get(k, 0.0), 1.05 * err1.get(k, 0.0))
+        assert err[k] <= bound, f"{cid}: {k} error {err[k]:.3e} > {bound:.3e} (gpu {err}, fp32 {ref32}); {diag}"
+    # the two runs side by side: where no BT branch differs, only the shards' summation order separates them
+    if not flip.any():
+        assert _rel(ybs, single[2]) <= 2e-5, diag
     # where the two runs' BT branches differ, both norms are within rounding of tau
     if flip.any():
         dist_tau = np.maximum(np.abs(n1[flip] - tau), np.abs(ns[flip] - tau)) / tau

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--chunks", default="16,24,32,48,64")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--streams", default="1,2")
     a = ap.parse_args()
     cfg = synth.CONFIGS["c4"]
     M, N, P, K = cfg["M"], cfg["N"], cfg["P"], cfg["K"]
@@ -38,26 +39,27 @@ def main():
     h = torch.from_numpy(synth.gaussian_psf(*cfg["psf"])).to(dev)
     planes = y.shape[0]
     out = torch.empty_like(y)
-    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(device=dev)]
+    nsmax = max(int(v) for v in a.streams.split(","))
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(nsmax - 1)]
     ws = [admm_deconv.Workspace() for _ in streams]
 
     def solve(c, nstreams):
         if c >= planes:
             admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws[0], stream=streams[0])
             return
-        if nstreams > 1:
-            streams[1].wait_stream(streams[0])
+        for k in range(1, nstreams):
+            streams[k].wait_stream(streams[0])
         for i, p0 in enumerate(range(0, planes, c)):
             si = i % nstreams
             admm_deconv.tvd_fft(y[p0:p0 + c], synth.LAMBDA, synth.RHO, h, False, K, out=out[p0:p0 + c],
                                 workspace=ws[si], stream=streams[si])
-        if nstreams > 1:
-            streams[0].wait_stream(streams[1])
+        for k in range(1, nstreams):
+            streams[0].wait_stream(streams[k])
 
     solve(planes, 1)
     torch.cuda.synchronize()
     ref = out.clone()
-    variants = [(planes, 1)] + [(int(c), ns) for c in a.chunks.split(",") for ns in (1, 2)]
+    variants = [(planes, 1)] + [(int(c), int(ns)) for c in a.chunks.split(",") for ns in a.streams.split(",")]
     for c, ns in variants:
         solve(c, ns)   # warm-up (workspace sizes, kernel attributes)
         torch.cuda.synchronize()
