@@ -21,10 +21,11 @@ ADMM_E_REDUCER = -5
 
 # library options (admm_set_option, include/admm_deconv.h)
 OPT_FUSED, OPT_FUSED_ADJ, OPT_LINE_T, OPT_COL_THREADS, OPT_GEN_TM, OPT_GEN_KN, OPT_PLANE_STAGGER, OPT_SMOOTH, OPT_RESIDENT, \
-    OPT_MIN_PLANES = range(10)
+    OPT_MIN_PLANES, OPT_MALL_STREAMS = range(11)
 OPTIONS = {"FUSED": OPT_FUSED, "FUSED_ADJ": OPT_FUSED_ADJ, "LINE_T": OPT_LINE_T, "COL_THREADS": OPT_COL_THREADS,
            "GEN_TM": OPT_GEN_TM, "GEN_KN": OPT_GEN_KN, "PLANE_STAGGER": OPT_PLANE_STAGGER,
-           "SMOOTH": OPT_SMOOTH, "RESIDENT": OPT_RESIDENT, "MIN_PLANES": OPT_MIN_PLANES}
+           "SMOOTH": OPT_SMOOTH, "RESIDENT": OPT_RESIDENT, "MIN_PLANES": OPT_MIN_PLANES,
+           "MALL_STREAMS": OPT_MALL_STREAMS}
 
 K_SETUP, K_PREP, K_COLUMN, K_LINE, K_FINAL, K_NORM, K_PLANE, K_ADJ = range(8)
 KERNEL_CLASSES = {K_SETUP: "setup", K_PREP: "prep", K_COLUMN: "column", K_LINE: "line",
@@ -40,7 +41,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
-           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths",
+           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths", "admm_query_forward_schedule",
            "admm_path_name", "admm_ipc_get_handle", "admm_ipc_open", "admm_ipc_close")
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
@@ -159,6 +160,9 @@ def load():
     L.admm_ipc_close.argtypes = [c_void_p, c_int]
     L.admm_query_paths.restype = c_int
     L.admm_query_paths.argtypes = [c_int] * 4 + [ctypes.c_longlong] + [c_int] * 4 + [ctypes.POINTER(c_int)] * 2
+    L.admm_query_forward_schedule.restype = c_int
+    L.admm_query_forward_schedule.argtypes = [c_int] * 4 + [ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong),
+                                              ctypes.POINTER(c_int)]
     L.admm_path_name.restype = ctypes.c_char_p
     L.admm_path_name.argtypes = [c_int]
     _lib = L
@@ -203,6 +207,13 @@ def query_paths(M, N, iso=False, kh=0, mode=MODE_FORWARD, flags=0, want_hbar=Fal
     check(L.admm_query_paths(M, N, int(iso), kh, int(planes), mode, flags, int(want_hbar), int(want_rho),
                              ctypes.byref(f), ctypes.byref(b)))
     return L.admm_path_name(f.value).decode(), (L.admm_path_name(b.value).decode() if b.value else None)
+
+
+def forward_schedule(M, N, iso=False, kh=0, planes=1):
+    """admm_query_forward_schedule: (planes per launch, streams) of a forward over `planes` planes."""
+    c, n = ctypes.c_longlong(0), ctypes.c_int(0)
+    check(load().admm_query_forward_schedule(M, N, int(iso), kh, int(planes), ctypes.byref(c), ctypes.byref(n)))
+    return c.value, n.value
 
 
 def copy_async(dst, src, nbytes, stream):

@@ -73,7 +73,7 @@ int admm_tvd_workspace_bytes(int M, int N, int P, int B, int kh, int kw, int iso
     if (!out_bytes) return fail(ADMM_E_INVALID, "out_bytes is NULL");
     int rc = check_shape(M, N, P, B, kh, kw, iso);
     if (rc) return rc;
-    *out_bytes = make_layout(M, N, chunk_planes((size_t)P * B, iso != 0), kh > 0, iso != 0).total;
+    *out_bytes = forward_ws_bytes(M, N, (size_t)P * B, kh, iso != 0);
     return ADMM_OK;
 }
 
@@ -187,6 +187,32 @@ int check_lam_rho(float lambda, float rho) {
     return ADMM_OK;
 }
 
+// Library streams of the MALL-resident schedule: created once per device, never destroyed (non-blocking; the
+// forward orders them against the caller's stream with events).
+hipStream_t lib_stream(int i) {
+    static std::mutex mu;
+    static std::vector<std::vector<hipStream_t>> pool;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)pool.size() <= dev) pool.resize(dev + 1);
+    auto& v = pool[dev];
+    while ((int)v.size() <= i) {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        v.push_back(st);
+    }
+    return v[i];
+}
+
+// forward workspace: one chunk layout, or one per stream of the MALL-resident schedule
+size_t forward_ws_bytes(int M, int N, size_t planes, int kh, bool iso, const PathPlan* plp) {
+    const PathPlan pl = plp ? *plp : plan_paths({M, N, iso, kh > 0, ADMM_MODE_FORWARD, 0, false, false, planes});
+    const ChunkPlan cp = forward_chunks(M, N, planes, iso, pl.fwd);
+    const size_t one = make_layout(M, N, cp.chunk, kh > 0, iso).total;
+    return cp.streams > 1 ? (size_t)cp.streams * align_up(one) : one;
+}
+
 int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const float* h, int kh, int kw,
                  const admm::ScalarSrc& sc, int iso, int maxit, void* workspace, size_t workspace_bytes, void* stream,
                  const admm_batch_reducer* reducer) {
@@ -197,22 +223,69 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     rc = check_common(y, x_out, maxit);
     if (rc) return rc;
     const size_t planes = (size_t)P * B;
-    const size_t chunk = chunk_planes(planes, iso != 0);   // an isotropic batch is one chunk
-    const Layout lay = make_layout(M, N, chunk, kh > 0, iso != 0);
-    rc = check_ws(workspace, workspace_bytes, lay.total);
-    if (rc) return rc;
-    rec_forget(workspace);   // whatever was recorded there is overwritten now
-    Launcher ln{reinterpret_cast<hipStream_t>(stream), g_prof.on, {}};
-    const size_t MN = (size_t)M * N;
     // a sharded isotropic solve plans without the plane-count rule: every shard must take the same path, since
     // the fused and 2-pass kernels hand the reducer their sum maps in different layouts (lane-native float2 vs
     // natural), and uneven shards can fall on either side of a threshold
     const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false, red ? 0 : planes});
-    for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
-        rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
-                         maxit, static_cast<unsigned char*>(workspace), lay, Traj{}, red, pl.fwd);
-    int rc2 = ln.finish();
-    return rc ? rc : rc2;
+    const ChunkPlan cp = forward_chunks(M, N, planes, iso != 0, pl.fwd);
+    const size_t chunk = cp.chunk;   // an isotropic batch is one chunk
+    const Layout lay = make_layout(M, N, chunk, kh > 0, iso != 0);
+    rc = check_ws(workspace, workspace_bytes, forward_ws_bytes(M, N, planes, kh, iso != 0, &pl));
+    if (rc) return rc;
+    rec_forget(workspace);   // whatever was recorded there is overwritten now
+    const hipStream_t s0 = reinterpret_cast<hipStream_t>(stream);
+    const size_t MN = (size_t)M * N;
+    unsigned char* ws = static_cast<unsigned char*>(workspace);
+    if (cp.streams <= 1) {
+        Launcher ln{s0, g_prof.on, {}};
+        for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
+            rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
+                             maxit, ws, lay, Traj{}, red, pl.fwd);
+        int rc2 = ln.finish();
+        return rc ? rc : rc2;
+    }
+    // MALL-resident schedule: chunk i on stream i mod n (the caller's stream and n - 1 library streams), each stream
+    // with its own chunk workspace; fork and join through events on the caller's stream
+    const int n = cp.streams;
+    const size_t stride = align_up(lay.total);
+    std::vector<Launcher> lns;
+    lns.reserve(n);
+    lns.push_back(Launcher{s0, g_prof.on, {}});
+    hipEvent_t fork = nullptr;
+    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess || hipEventRecord(fork, s0) != hipSuccess)
+        return fail(ADMM_E_HIP, "MALL schedule: fork event");
+    for (int k = 1; k < n; ++k) {
+        hipStream_t sk = lib_stream(k - 1);
+        if (!sk || hipStreamWaitEvent(sk, fork, 0) != hipSuccess) {
+            hipEventDestroy(fork);
+            return fail(ADMM_E_HIP, "MALL schedule: library stream %d", k);
+        }
+        lns.push_back(Launcher{sk, g_prof.on, {}});
+    }
+    hipEventDestroy(fork);   // (released once the waits have consumed it)
+    size_t i = 0;
+    for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk, ++i) {
+        const int k = (int)(i % (size_t)n);
+        rc = run_forward(lns[k], y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
+                         maxit, ws + (size_t)k * stride, lay, Traj{}, red, pl.fwd);
+    }
+    // join: the caller's stream waits for every library stream (also after an error, so nothing is left running
+    // against the caller's buffers unordered)
+    for (int k = 1; k < n; ++k) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(e, lns[k].s) != hipSuccess || hipStreamWaitEvent(s0, e, 0) != hipSuccess)
+                rc = rc ? rc : fail(ADMM_E_HIP, "MALL schedule: join");
+            hipEventDestroy(e);
+        } else if (!rc) {
+            rc = fail(ADMM_E_HIP, "MALL schedule: join event");
+        }
+    }
+    for (auto& l : lns) {
+        const int r2 = l.finish();
+        if (!rc) rc = r2;
+    }
+    return rc;
 }
 
 // phases: 1 = forward recording the trajectory into the workspace (writes x_out), 2 = reverse sweep

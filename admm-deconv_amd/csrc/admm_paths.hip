@@ -17,7 +17,7 @@ namespace admm_capi {
 // Library options (admm_set_option; process-global, read at each call).  The defaults are the tuned
 // choices; the others exist for tests (fused vs 2-pass) and tuning experiments.  A recording stores
 // the option values it was made with, and its replay rejects a change (RecTag below).
-std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {-1}};
+std::atomic<int> g_opt[ADMM_OPT_COUNT] = {{1}, {1}, {0}, {0}, {0}, {0}, {0}, {1}, {1}, {-1}, {4}};
 int opt(int k) { return g_opt[k].load(std::memory_order_relaxed); }
 
 // ADMM_OPT_FUSED = 0 forces the 2-pass path (tests compare the two).
@@ -94,6 +94,25 @@ bool enough_planes(const PathIn& q, MinPlanesFor which) {
     }
     return true;
 }
+// MALL-resident schedule (ADMM_OPT_MALL_STREAMS; DESIGN.md s5 "Round 6, c4").  A 2-pass iteration touches
+// 28 B/px (packed spectrum in and out 8, s in and out 16, Y_h 4): at c4 (768 planes of 512^2) 5.6 GB per
+// iteration, so every pass streams from HBM.  Chunks of ~224 MiB / n (8 planes at 512^2, n = 4) run all K
+// iterations with n of them in flight: their sets stay in the 256 MiB Infinity Cache, and the n streams overlap
+// each other's kernel tails.  tools/c4_chunk_probe.py, profiles/r06_c4_chunk_probe.jsonl: 81.8 -> 75.7 ms per c4
+// solve (8 planes x 4 streams; 16 x 2 77.2, 8 x 2 97.8: one or two small grids alone leave the chip idle).
+ChunkPlan forward_chunks(int M, int N, size_t planes, bool iso, int fwd_path) {
+    const size_t base = chunk_planes(planes, iso);
+    const int n = opt(ADMM_OPT_MALL_STREAMS);
+    if (iso || n <= 1 || fwd_path != ADMM_PATH_2PASS) return {base, 1};
+    constexpr size_t kMall = size_t(256) << 20, kBudget = size_t(224) << 20;
+    const size_t per_plane = 28 * (size_t)M * N;
+    if (planes * per_plane <= 2 * kMall) return {base, 1};
+    size_t chunk = kBudget / ((size_t)n * per_plane);
+    if (chunk < 1) chunk = 1;
+    if (chunk > base) chunk = base;
+    return {chunk, n > 16 ? 16 : n};
+}
+
 // Several 256 x 256 branches in one grid (admm_tvd_forward_multi_dev_f32): the per-plane kernels from the fused
 // paths' plane counts in all (kMinFused / kMinFusedIso), below them the 2-pass kernels over every branch's planes
 // (the c5 training step at batch 2 has 30: tools/small_batch_probe.py, profiles/r05_small_batch_probe.jsonl).
@@ -239,6 +258,19 @@ int admm_query_paths(int M, int N, int iso, int kh, long long planes, int mode, 
     const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, mode, flags, want_hbar != 0, want_rho != 0, (size_t)planes});
     *fwd_path = pl.fwd;
     *bwd_path = pl.bwd;
+    return ADMM_OK;
+}
+
+int admm_query_forward_schedule(int M, int N, int iso, int kh, long long planes, long long* chunk_planes,
+                                int* streams) {
+    if (!chunk_planes || !streams) return fail(ADMM_E_INVALID, "admm_query_forward_schedule: NULL output");
+    const int rc = check_shape(M, N, 1, 1, kh, kh, iso);
+    if (rc) return rc;
+    if (planes <= 0) return fail(ADMM_E_INVALID, "admm_query_forward_schedule: planes must be > 0");
+    const PathPlan pl = plan_paths({M, N, iso != 0, kh > 0, ADMM_MODE_FORWARD, 0, false, false, (size_t)planes});
+    const ChunkPlan cp = forward_chunks(M, N, (size_t)planes, iso != 0, pl.fwd);
+    *chunk_planes = (long long)std::min(cp.chunk, (size_t)planes);
+    *streams = cp.streams;
     return ADMM_OK;
 }
 

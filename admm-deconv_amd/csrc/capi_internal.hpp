@@ -124,6 +124,20 @@ inline size_t launch_planes(size_t planes) { return planes < kChunkPlanes ? plan
 // batch is never split: it runs as one launch sequence of up to 65535 planes (check_shape's limit).
 inline size_t chunk_planes(size_t planes, bool iso) { return iso ? planes : launch_planes(planes); }
 
+// MALL-resident schedule of the anisotropic 2-pass forward (ADMM_OPT_MALL_STREAMS, DESIGN.md s5 "Round 6, c4"):
+// planes in chunks of `chunk`, `streams` chunks in flight (the caller's stream + library streams), each chunk's
+// per-iteration working set kept in the 256 MiB Infinity Cache.  streams = 1: the plain chunking above.
+struct ChunkPlan {
+    size_t chunk;
+    int streams;
+};
+ChunkPlan forward_chunks(int M, int N, size_t planes, bool iso, int fwd_path);
+// the library's own streams on the current device (created once; non-blocking)
+hipStream_t lib_stream(int i);
+struct PathPlan;
+// forward workspace bytes (one chunk layout, or one per stream of the MALL-resident schedule)
+size_t forward_ws_bytes(int M, int N, size_t planes, int kh, bool iso, const PathPlan* pl = nullptr);
+
 // Trajectory recorded by the forward for the backward (all optional).
 struct Traj {
     float* s = nullptr;      // (K-1) x planes x 2 x M x N : s_k for k = 1..K-1

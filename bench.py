@@ -559,6 +559,8 @@ def main():
         admm_deconv.tvd_fft(y, synth.LAMBDA, synth.RHO, h, False, K, out=out, workspace=ws[0], stream=stream)
     _lib.profile_enable(False)
     planes = B * P
+    # planes per launch: the MALL-resident schedule runs large 2-pass batches as chunks on several streams
+    chunk, nstreams = _lib.forward_schedule(M, N, False, cfg["psf"][0], planes)
     kb = kernel_bytes_per_plane(M, N, K)
     kernels = {}
     for cls, name in _lib.KERNEL_CLASSES.items():
@@ -568,12 +570,12 @@ def main():
         avg_ms = ms / n
         e = {"launches_per_solve": n // reps, "avg_ms": avg_ms, "total_ms_per_solve": ms / reps}
         if name in kb:
-            e["algorithmic_bytes_per_launch"] = kb[name] * planes
-            e["achieved_GBps"] = kb[name] * planes / (avg_ms * 1e-3) / 1e9
+            e["algorithmic_bytes_per_launch"] = kb[name] * chunk
+            e["achieved_GBps"] = kb[name] * chunk / (avg_ms * 1e-3) / 1e9
         kernels[name] = e
     dom = max((k for k in kernels if k in kb), key=lambda k: kernels[k]["total_ms_per_solve"])
     alg_bytes = kb["plane"] * planes if "plane" in kernels else canonical_bytes(M, N, K) * planes
-    traffic = load_traffic(config, dom, planes=planes)
+    traffic = load_traffic(config, dom, planes=chunk)
     ach = kernels[dom]["achieved_GBps"]
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -583,7 +585,13 @@ def main():
         "frac_of_achievable": round(ach / achievable_gbs(), 4) if achievable_gbs() else None,
         "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes_per_launch"],
         "avg_launch_ms": round(kernels[dom]["avg_ms"], 5),
-        "compute": compute_side(config, dom, kernels[dom]["avg_ms"], planes),
+        "compute": compute_side(config, dom, kernels[dom]["avg_ms"], chunk),
+        # launches of `chunk_planes` planes; with streams > 1 that many chunks' launches run concurrently, so a
+        # launch's duration includes its share of the chip (the whole-solve figure below is the aggregate)
+        # (rocprofv3's begin -> end of the same launches is shorter: profiles/r06_c4_mall_kernel_stats.csv, DESIGN.md
+        # s5); overlap = the kernels' event time per solve over the solve's wall time
+        "schedule": {"chunk_planes": chunk, "streams": nstreams,
+                     "overlap": round(sum(k["total_ms_per_solve"] for k in kernels.values()) / ms_per_step, 2)},
         "whole_solve": {
             # the bytes of the path that ran (fused: plane_bytes_per_px; 2-pass: SURVEY s8d canonical)
             "algorithmic_bytes": alg_bytes,

@@ -256,7 +256,13 @@ enum {
                                     runs the 2-pass kernels, so a plane's result can differ by fp32 rounding
                                     between batch sizes); 0: those paths at every batch size (results independent
                                     of the batch size, as for anisotropic solves before); n > 0: from n planes  */
-    ADMM_OPT_COUNT = 10
+    ADMM_OPT_MALL_STREAMS = 10,  /* 4 (default): an anisotropic 2-pass forward whose per-iteration working set
+                                    (28 B/px: spectrum in / out, s in / out, Y_h) is over twice the 256 MiB
+                                    Infinity Cache runs as plane chunks of ~224 MiB / n, n chunks at a time on
+                                    the caller's stream and n - 1 library streams (each chunk all K iterations,
+                                    its set cache-resident; bitwise the whole-batch solve; workspace n chunks);
+                                    0 or 1: the whole batch on the caller's stream                           */
+    ADMM_OPT_COUNT = 11
 };
 int admm_set_option(int option, int value);
 int admm_get_option(int option, int* value);
@@ -290,6 +296,12 @@ enum {
 int admm_query_paths(int M, int N, int iso, int kh, long long planes, int mode, int flags, int want_hbar, int want_rho,
                      int* fwd_path, int* bwd_path);
 const char* admm_path_name(int path);
+/* The forward's plane schedule for a call of `planes` = P*B planes (host only, ADMM_OPT_MALL_STREAMS): the planes
+ * per launch (*chunk_planes) and the number of streams the chunks run on (*streams; 1 = the caller's stream only,
+ * chunks back to back).  For tests and tooling, e.g. to price one launch's bytes.  ADMM_E_INVALID as
+ * admm_query_paths. */
+int admm_query_forward_schedule(int M, int N, int iso, int kh, long long planes, long long* chunk_planes,
+                                int* streams);
 
 /* Output transport of the batch-sharded solve (BASELINE c3; the reference gathers nothing -- its batch
  * lives on one device, ops.jl:168-173): an asynchronous copy of `bytes` from src to dst on `stream`, both

@@ -62,6 +62,30 @@ def test_isotropic_batch_is_never_chunked():
     assert _lib.workspace_bytes(4, 4, 1, 65300, 0, 0, False) == _lib.workspace_bytes(4, 4, 1, chunk, 0, 0, False)
 
 
+def test_mall_resident_schedule():
+    """ADMM_OPT_MALL_STREAMS (admm_paths.hip forward_chunks): an anisotropic 2-pass batch whose 28 B/px per-iteration
+    set exceeds 512 MiB runs as ~224 MiB / n chunks on n streams, with one chunk workspace per stream; c4 (768
+    planes of 512^2) is 8 planes x 4 streams.  Smaller batches, isotropic ones and the other paths are one stream."""
+    assert _lib.get_option("MALL_STREAMS") == 4
+    assert _lib.forward_schedule(512, 512, False, 15, 768) == (8, 4)
+    assert _lib.forward_schedule(512, 512, False, 15, 60) == (60, 1)         # 420 MB: one stream
+    assert _lib.forward_schedule(512, 512, True, 15, 768) == (768, 1)        # the prox couples the batch
+    assert _lib.forward_schedule(1024, 1024, False, 0, 64) == (2, 4)
+    assert _lib.forward_schedule(256, 256, False, 15, 4096)[1] == 1          # the fused path
+    w4 = _lib.workspace_bytes(512, 512, 3, 256, 15, 15, False)
+    with _lib.option("MALL_STREAMS", 1):
+        assert _lib.forward_schedule(512, 512, False, 15, 768) == (768, 1)
+        w1 = _lib.workspace_bytes(512, 512, 3, 256, 15, 15, False)
+        one = _lib.workspace_bytes(512, 512, 1, 8, 15, 15, False)
+    with _lib.option("MALL_STREAMS", 2):
+        assert _lib.forward_schedule(512, 512, False, 15, 768) == (16, 2)
+    assert w4 >= 4 * one and w4 < 4 * one + 4 * 4096 and w4 < w1 / 20
+    L = _lib.load()
+    c, n = ctypes.c_longlong(0), ctypes.c_int(0)
+    assert L.admm_query_forward_schedule(512, 512, 0, 15, 0, ctypes.byref(c), ctypes.byref(n)) == _lib.ADMM_E_INVALID
+    assert L.admm_query_forward_schedule(512, 512, 0, 15, 8, None, ctypes.byref(n)) == _lib.ADMM_E_INVALID
+
+
 @pytest.mark.parametrize("args,code", [
     ((8192, 64, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # M too large
     ((64, 8192, 1, 1, 5, 5, 0), _lib.ADMM_E_UNSUPPORTED),  # N too large
