@@ -99,16 +99,21 @@ bool enough_planes(const PathIn& q, MinPlanesFor which) {
 // iteration, so every pass streams from HBM.  Chunks of ~224 MiB / n (8 planes at 512^2, n = 4) run all K
 // iterations with n of them in flight: their sets stay in the 256 MiB Infinity Cache, and the n streams overlap
 // each other's kernel tails.  tools/c4_chunk_probe.py, profiles/r06_c4_chunk_probe.jsonl: 81.8 -> 75.7 ms per c4
-// solve (8 planes x 4 streams; 16 x 2 77.2, 8 x 2 97.8: one or two small grids alone leave the chip idle).
+// solve (8 planes x 4 streams; 16 x 2 77.2, 8 x 2 97.8: one or two small grids alone leave the chip idle; more
+// than 4 streams share the process's 4 hardware queues: 5-12 streams 97-149 ms, profiles/r06_c4_mall_streams_sweep.txt).
+// The smooth-length 2-pass kernels gain the same way (480 x 640 x 64 / 256 +5 / +7 %, 384^2 x 512 +11 %).
 ChunkPlan forward_chunks(int M, int N, size_t planes, bool iso, int fwd_path) {
     const size_t base = chunk_planes(planes, iso);
     const int n = opt(ADMM_OPT_MALL_STREAMS);
-    if (iso || n <= 1 || fwd_path != ADMM_PATH_2PASS) return {base, 1};
+    const bool two_pass = fwd_path == ADMM_PATH_2PASS || fwd_path == ADMM_PATH_SMOOTH || fwd_path == ADMM_PATH_RUNTIME;
+    if (iso || n <= 1 || !two_pass) return {base, 1};
     constexpr size_t kMall = size_t(256) << 20, kBudget = size_t(224) << 20;
     const size_t per_plane = 28 * (size_t)M * N;
     if (planes * per_plane <= 2 * kMall) return {base, 1};
     size_t chunk = kBudget / ((size_t)n * per_plane);
-    if (chunk < 1) chunk = 1;
+    // chunks of 1-2 large planes lose (2048^2 x 8: 1-plane chunks -15 %, 1000^2 x 64: 2-plane chunks -2 %;
+    // profiles/r06_mall_generic_ab.jsonl): whole batch
+    if (chunk < 4) return {base, 1};
     if (chunk > base) chunk = base;
     return {chunk, n > 16 ? 16 : n};
 }

@@ -256,11 +256,13 @@ enum {
                                     runs the 2-pass kernels, so a plane's result can differ by fp32 rounding
                                     between batch sizes); 0: those paths at every batch size (results independent
                                     of the batch size, as for anisotropic solves before); n > 0: from n planes  */
-    ADMM_OPT_MALL_STREAMS = 10,  /* 4 (default): an anisotropic 2-pass forward whose per-iteration working set
-                                    (28 B/px: spectrum in / out, s in / out, Y_h) is over twice the 256 MiB
-                                    Infinity Cache runs as plane chunks of ~224 MiB / n, n chunks at a time on
-                                    the caller's stream and n - 1 library streams (each chunk all K iterations,
-                                    its set cache-resident; bitwise the whole-batch solve; workspace n chunks);
+    ADMM_OPT_MALL_STREAMS = 10,  /* 4 (default): an anisotropic 2-pass forward (power-of-two, smooth or runtime
+                                    lengths) whose per-iteration working set (28 B/px: spectrum in / out, s in /
+                                    out, Y_h) is over twice the 256 MiB Infinity Cache runs as plane chunks of
+                                    ~224 MiB / n (at least 4 planes, else the whole batch), n chunks at a time
+                                    on the caller's stream and n - 1 library streams (each chunk all K
+                                    iterations, its set cache-resident; bitwise the whole-batch solve;
+                                    workspace n chunks; admm_query_forward_schedule);
                                     0 or 1: the whole batch on the caller's stream                           */
     ADMM_OPT_COUNT = 11
 };

@@ -65,12 +65,15 @@ def test_isotropic_batch_is_never_chunked():
 def test_mall_resident_schedule():
     """ADMM_OPT_MALL_STREAMS (admm_paths.hip forward_chunks): an anisotropic 2-pass batch whose 28 B/px per-iteration
     set exceeds 512 MiB runs as ~224 MiB / n chunks on n streams, with one chunk workspace per stream; c4 (768
-    planes of 512^2) is 8 planes x 4 streams.  Smaller batches, isotropic ones and the other paths are one stream."""
+    planes of 512^2) is 8 planes x 4 streams.  Smaller batches, chunks under 4 planes, isotropic batches and the
+    one-workgroup-per-plane paths are one stream."""
     assert _lib.get_option("MALL_STREAMS") == 4
     assert _lib.forward_schedule(512, 512, False, 15, 768) == (8, 4)
     assert _lib.forward_schedule(512, 512, False, 15, 60) == (60, 1)         # 420 MB: one stream
     assert _lib.forward_schedule(512, 512, True, 15, 768) == (768, 1)        # the prox couples the batch
-    assert _lib.forward_schedule(1024, 1024, False, 0, 64) == (2, 4)
+    assert _lib.forward_schedule(1024, 1024, False, 0, 64) == (64, 1)       # 2-plane chunks would lose
+    assert _lib.forward_schedule(640, 480, False, 15, 64) == (6, 4)          # the smooth-length kernels too
+    assert _lib.forward_schedule(250, 250, False, 15, 256)[1] == 1           # the CU-resident path
     assert _lib.forward_schedule(256, 256, False, 15, 4096)[1] == 1          # the fused path
     w4 = _lib.workspace_bytes(512, 512, 3, 256, 15, 15, False)
     with _lib.option("MALL_STREAMS", 1):

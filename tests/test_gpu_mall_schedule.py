@@ -56,6 +56,22 @@ def test_mall_schedule_bitwise_one_stream(dev, planes):
     assert_parity(x4[:2].cpu().numpy(), ref, what="mall schedule 512^2")
 
 
+def test_mall_schedule_smooth_lengths(dev):
+    """480 x 640 x 64 runs the smooth-length 2-pass kernels in 6-plane chunks on 4 streams: bitwise the whole batch."""
+    N, M, B, K = 480, 640, 64, 4
+    assert _lib.query_paths(M, N, False, 15, planes=B)[0] == "smooth"
+    assert _lib.forward_schedule(M, N, False, 15, B) == (6, 4)
+    h = synth.gaussian_psf(15, 2.5)
+    base = synth.make_batch(8, M, N, h, g0=3)
+    y = torch.from_numpy(np.concatenate([base] * 8)).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    x4, s4 = _solve(dev, y, ht, K, 4)
+    x1, s1 = _solve(dev, y, ht, K, 1)
+    assert torch.equal(x4, x1) and s4 == s1
+    ref = oracle_solve(base[:1], LAM, RHO, h, False, K, "spectral", what="mall 480x640")
+    assert_parity(x4[:1].cpu().numpy(), ref, what="mall schedule 480x640")
+
+
 def test_mall_schedule_under_graph_capture(dev):
     """The fork / join events are graph nodes: a captured call replays to the eager result."""
     M, K, planes = 512, 4, 80

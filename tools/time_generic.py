@@ -50,7 +50,8 @@ def main():
             if n:
                 ks[name] = round(ms, 3)
         r = {"shape": [N, M], "batch": B, "K": K, "ms": round(1000 * dt, 3), "img_s": round(B / dt, 1),
-             "canonical_GBps": round(canon / dt / 1e9, 1), "kernel_ms": ks}
+             "canonical_GBps": round(canon / dt / 1e9, 1), "kernel_ms": ks,
+             "path": _lib.query_paths(M, N, False, 15, planes=B)[0], "schedule": _lib.forward_schedule(M, N, False, 15, B)}
         print(json.dumps(r), flush=True)
         out.append(r)
     os.makedirs("gpurun_out", exist_ok=True)
