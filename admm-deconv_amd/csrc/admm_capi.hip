@@ -416,7 +416,7 @@ MultiLayout make_multi_layout(size_t planes, int nbr, int maxit, int flags) {
         return L;
     }
     L.F = take((size_t)nbr * multi_F_bytes());
-    L.hln = take(planes * MN * 4);
+    L.hln = take(admm::plane::hty_bytes(planes));   // lane-native H^T y at its skewed plane stride
     L.sln = take(planes * MN * 8);
     if (rec) {
         L.traj = take((size_t)(K > 1 ? K - 1 : 1) * planes * (masks ? MN / 2 : MN * 8));

@@ -55,7 +55,9 @@ inline Layout make_layout(int M, int N, size_t planes, bool psf, bool iso) {
     L.sB = take(planes * 2 * MN * 4);
     // N lines x M/2 complex (packed) -- or M/2 + 1 bins per line on the generic path
     const size_t spec_bytes = generic_shape(M, N) ? planes * (size_t)(M / 2 + 1) * N * 8 : planes * MN * 4;
-    L.spec0 = take(spec_bytes);
+    // the fused 256^2 kernels keep their lane-native H^T y in spec0, at a skewed plane stride
+    L.spec0 = take(fused_tables_shape(M, N) && admm::plane::hty_bytes(planes) > spec_bytes ? admm::plane::hty_bytes(planes)
+                                                                                            : spec_bytes);
     L.spec1 = take(spec_bytes);
     L.xg = generic_shape(M, N) ? take(planes * MN * 4) : 0;
     L.fmap = iso ? take(MN * 4) : 0;

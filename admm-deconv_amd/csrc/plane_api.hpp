@@ -43,6 +43,12 @@ constexpr int kTabEntries = 2 * 32 * 512;   // lane-native spectral table entrie
 
 // bytes of the lane-native tables (Cf, C0b, Gf, G0b) carved from the workspace
 inline size_t tables_bytes() { return (size_t)kTabEntries * 12 + 256 * 12 + 256; }
+// Plane stride of the lane-native H^T y (float2 units): 256 KiB + 1 KiB.  At a power-of-two stride every
+// workgroup's row phase, in lock-step with the others, reads H^T y at the same offset of its own plane; the
+// 1 KiB skew spreads those reads over the memory channels: c2 164k -> 168-170k, c3's 256-plane shard
+// 149-151k -> 157-158k img/s (profiles/r06_plane_pad_ab*.jsonl; the s state's stride showed no such effect).
+constexpr size_t kHtyStrideF2 = 64 * 512 + 128;
+inline size_t hty_bytes(size_t planes) { return planes * kHtyStrideF2 * 8; }
 
 // Cf/C0b/Gf/G0b from the 2-pass tables Ct/Gt (Gt may be NULL: no PSF)
 hipError_t launch_tables(const float* Ct, const float2* Gt, void* tables, hipStream_t s);

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kPT) void plane256_iso_kernel(const float* __restri
         tw[q * kTQ + kk] = make_float2((float)cs, (float)-sn);
     }
     constexpr unsigned kS4 = 64 * kPT * 16, kS2 = 64 * kPT * 8;
-    const rsrc_t hp = make_rsrc(hln + plane * 64 * kPT, kS2);
+    const rsrc_t hp = make_rsrc(hln + plane * kHtyStrideF2, kS2);
     const rsrc_t sp = make_rsrc(s_in + plane * 64 * kPT, kS4);        // s_k (k > 0)
     const rsrc_t so = make_rsrc(s_out + plane * 64 * kPT, kS4);       // s_{k+1}: in place, or the next trajectory slot
     const rsrc_t fp = make_rsrc(fmap, kS2);

@@ -613,7 +613,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     float2 S[64];
 #pragma unroll
     for (int n = 0; n < 64; ++n) S[n] = yrow[2 * n + hb];
-    const rsrc_t hp = make_rsrc(hln + plane * 64 * kPT, 64 * kPT * 8);
+    const rsrc_t hp = make_rsrc(hln + plane * kHtyStrideF2, 64 * kPT * 8);
     const rsrc_t sp = make_rsrc(sln + plane * 64 * kPT, 64 * kPT * 16);
     const rsrc_t cfr = make_rsrc(Cf, kTab * 4);
     const rsrc_t gfr = make_rsrc(Gf, PSF ? kTab * 8 : 0);

@@ -28,7 +28,7 @@ C0b = torch.zeros(256, device=dev)
 assert lib.devtest_plane_tables(Ct.data_ptr(), Cf.data_ptr(), C0b.data_ptr()) == 0
 y = torch.from_numpy(synth.make_batch(8, M, N, None)).to(dev).repeat(B // 8, 1, 1, 1).contiguous()
 x = torch.zeros_like(y)
-hln = torch.zeros(B * 64 * 512 * 2, device=dev)
+hln = torch.zeros(B * (64 * 512 + 128) * 2, device=dev)   # plane_api.hpp kHtyStrideF2
 sln = torch.zeros(B * 64 * 512 * 4, device=dev)
 dbg = torch.zeros(B * 8 * 512, dtype=torch.int64, device=dev)
 for rep in range(3):
