@@ -38,7 +38,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_tvd_forward_record_f32", "admm_tvd_backward_recorded_f32",
            "admm_tvd_forward_dev_f32", "admm_tvd_backward_dev_f32", "admm_tvd_forward_record_dev_f32",
            "admm_tvd_backward_recorded_dev_f32", "admm_set_option", "admm_get_option",
-           "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_ssim_f32", "admm_mse_f32",
+           "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_gmsd_backward_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
            "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths", "admm_query_forward_schedule",
@@ -138,6 +138,9 @@ def load():
     L.admm_gmsd_f32.restype = c_int
     L.admm_gmsd_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [c_float, c_float, c_void_p, c_void_p, c_void_p,
                                                                      c_void_p, c_size_t, c_void_p]
+    L.admm_gmsd_backward_f32.restype = c_int
+    L.admm_gmsd_backward_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [c_float, c_float, c_void_p, c_void_p,
+                                                                              c_void_p, c_size_t, c_void_p]
     L.admm_ssim_f32.restype = c_int
     L.admm_ssim_f32.argtypes = [c_void_p, c_void_p] + [c_int] * 4 + [ctypes.POINTER(c_float), c_int, c_float, c_int,
                                                                      c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,

@@ -69,16 +69,36 @@ def _gmsd_call(x4, y4, t, alpha, out_bar=None, want_grad=False):
 
 
 class _GmsdFn(torch.autograd.Function):
+    """The forward keeps its own workspace when x needs a gradient: it holds the per-block partial sums, from which
+    admm_gmsd_backward_f32 forms the gradient without re-running the forward kernel."""
+
     @staticmethod
     def forward(ctx, x4, y4, t, alpha):
         ctx.save_for_backward(x4, y4)
         ctx.t, ctx.alpha = t, alpha
-        return _gmsd_call(x4, y4, t, alpha)[0]
+        if not ctx.needs_input_grad[0]:
+            return _gmsd_call(x4, y4, t, alpha)[0]
+        B, C, N, M = x4.shape
+        nb = ctypes.c_size_t(0)
+        _lib.check(_lib.load().admm_metrics_workspace_bytes(M, N, C, B, 0, 1, ctypes.byref(nb)))
+        ctx.ws = Workspace()   # private: a second loss before backward must not overwrite these sums
+        wp, wl = ctx.ws.get(nb.value, x4.device, torch.cuda.current_stream(x4.device))
+        per = torch.empty(B, dtype=torch.float32, device=x4.device)
+        _lib.check(_lib.load().admm_gmsd_f32(x4.data_ptr(), y4.data_ptr(), M, N, C, B, float(t), float(alpha),
+                                             per.data_ptr(), None, None, wp, wl, _stream(x4.device)))
+        return per
 
     @staticmethod
     def backward(ctx, gper):
         x4, y4 = ctx.saved_tensors
-        _, xb = _gmsd_call(x4, y4, ctx.t, ctx.alpha, out_bar=gper, want_grad=True)
+        B, C, N, M = x4.shape
+        xb = torch.empty_like(x4)
+        ob = gper.contiguous().to(torch.float32)
+        wp, wl = ctx.ws.get(0, x4.device, torch.cuda.current_stream(x4.device))
+        _lib.check(_lib.load().admm_gmsd_backward_f32(x4.data_ptr(), y4.data_ptr(), M, N, C, B, float(ctx.t),
+                                                      float(ctx.alpha), ob.data_ptr(), xb.data_ptr(), wp, wl,
+                                                      _stream(x4.device)))
+        ctx.ws = None
         return xb, None, None, None
 
 

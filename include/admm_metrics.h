@@ -30,6 +30,14 @@ int admm_gmsd_f32(const float* x, const float* y, int M, int N, int C, int B, fl
                   float* out, const float* out_bar, float* x_bar, void* workspace,
                   size_t workspace_bytes, void* stream);
 
+/* The GMSD gradient without re-running the forward: `workspace` must hold what a preceding admm_gmsd_f32 call
+ * left there for the same x, y, sizes, t and alpha (its per-block partial sums; enqueued before this call on the
+ * same stream or ordered with it), and be at least admm_metrics_workspace_bytes(M, N, C, B, 0, 1) bytes.  x_bar
+ * = d(sum_b out_bar[b] out[b]) / dx (out_bar NULL: 1/B each, the mean). */
+int admm_gmsd_backward_f32(const float* x, const float* y, int M, int N, int C, int B, float t, float alpha,
+                           const float* out_bar, float* x_bar, void* workspace, size_t workspace_bytes,
+                           void* stream);
+
 /* SSIM per image: mean of the SSIM map with the separable window taps[0..ks) (host pointer, ks <= 15;
  * the reference's 11-tap Gaussian or a box), C1 = (0.01 peakval)^2, C2 = (0.03 peakval)^2; crop != 0:
  * valid window positions, else same-size on the symmetric padding (ssim.jl:99-108).  x_bar needs

@@ -118,3 +118,22 @@ def test_gmsd_on_two_streams_does_not_share_scratch(dev):
         torch.cuda.synchronize()
         for g, r in zip(got, ref):
             assert torch.equal(g, r)
+
+
+def test_gmsd_backward_from_the_forward_sums(dev):
+    """admm_gmsd_backward_f32 (the autograd backward) forms x_bar from the partial sums the forward left in its
+    private workspace: bitwise the one-call gradient (admm_gmsd_f32 with x_bar), also with a second GMSD loss
+    evaluated between the forward and the backward."""
+    from admm_deconv.metrics import _gmsd_call
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.random((3, 2, 40, 48), dtype=np.float32)).to(dev)
+    y = torch.from_numpy(rng.random((3, 2, 40, 48), dtype=np.float32)).to(dev)
+    w = torch.tensor([0.5, -1.0, 2.0], device=dev)
+    _, ref = _gmsd_call(x, y, 0.0026, 0.0, out_bar=w, want_grad=True)
+    xt = x.clone().requires_grad_(True)
+    per = metrics.gmsd(xt, y, reduction=lambda v: v)
+    other = metrics.gmsd(y.clone().requires_grad_(True), x, reduction=lambda v: v)   # overwrites shared scratch
+    (per * w).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(xt.grad, ref)
+    assert torch.isfinite(other).all()
