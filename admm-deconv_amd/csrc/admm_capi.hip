@@ -238,9 +238,10 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     unsigned char* ws = static_cast<unsigned char*>(workspace);
     if (cp.streams <= 1) {
         Launcher ln{s0, g_prof.on, {}};
+        // the tables (twiddles, C / G, scalars) once: later chunks reuse them from the same workspace
         for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk)
             rc = run_forward(ln, y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
-                             maxit, ws, lay, Traj{}, red, pl.fwd);
+                             maxit, ws, lay, Traj{}, red, pl.fwd, p0 == 0);
         int rc2 = ln.finish();
         return rc ? rc : rc2;
     }
@@ -266,8 +267,9 @@ int forward_impl(const float* y, float* x_out, int M, int N, int P, int B, const
     size_t i = 0;
     for (size_t p0 = 0; p0 < planes && rc == 0; p0 += chunk, ++i) {
         const int k = (int)(i % (size_t)n);
+        // each stream's chunk workspace builds the tables with its first chunk (96 setup launches per c4 solve -> 4)
         rc = run_forward(lns[k], y + p0 * MN, x_out + p0 * MN, M, N, std::min(chunk, planes - p0), h, kh, kw, sc, iso,
-                         maxit, ws + (size_t)k * stride, lay, Traj{}, red, pl.fwd);
+                         maxit, ws + (size_t)k * stride, lay, Traj{}, red, pl.fwd, i < (size_t)n);
     }
     // join: the caller's stream waits for every library stream (also after an error, so nothing is left running
     // against the caller's buffers unordered)

@@ -246,7 +246,7 @@ int run_resident_iso(Launcher& ln, int M, int N, size_t planes, const float* hty
 
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
                 int kw, const admm::ScalarSrc& sc, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                const Traj& tr, const admm_batch_reducer* red, int fwd_path) {
+                const Traj& tr, const admm_batch_reducer* red, int fwd_path, bool tables) {
     hipStream_t s = ln.s;
     int rc = ADMM_OK;
     const size_t MN = (size_t)M * N;
@@ -262,7 +262,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
     float* prm = reinterpret_cast<float*>(ws + lay.prm);   // tau = lambda / rho (ops.jl:20), rho, lambda
     double2* SigT = tr.sig;
 
-    rc = ln.run(ADMM_K_SETUP, [&] {
+    if (tables) rc = ln.run(ADMM_K_SETUP, [&] {
         const size_t lds = (size_t)(M + N) * 16 + (kh * kw <= admm::kSetupPsfLds ? (size_t)kh * kw * 4 : 0);
         const int nb = (int)(((size_t)(L + 1) * N + kThreads - 1) / kThreads);
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
@@ -285,11 +285,11 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         // one workgroup per plane runs all K iterations (plane_kernel.hip); lane-native H^T y in
         // spec0, lane-native s in sA -- or, recording a trajectory, s_k in its own slot of tr.s
         namespace pk = admm::plane;
-        void* tables = ws + lay.F;
-        rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, tables, s); });
+        void* ptab = ws + lay.F;
+        if (tables) rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, ptab, s); });
         if (rc) return rc;
         rc = ln.run(ADMM_K_PLANE, [&] {
-            return pk::launch_plane(y, x_out, tables, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
+            return pk::launch_plane(y, x_out, ptab, kh > 0, spec0, reinterpret_cast<float4*>(sbuf[0]), prm, maxit,
                                    planes, s, tr.m ? nullptr : reinterpret_cast<float4*>(tr.s), nullptr, tr.m);
         });
         return rc;
@@ -298,8 +298,8 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         // isotropic at 256 x 256: the split-iteration per-plane kernels (plane_iso.hip), the spectrum
         // resident in the CU; per iteration one plane256_iso_kernel and one iso_norm_kernel (batch norm)
         namespace pk = admm::plane;
-        void* tables = ws + lay.F;
-        rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, tables, s); });
+        void* ptab = ws + lay.F;
+        if (tables) rc = ln.run(ADMM_K_SETUP, [&] { return pk::launch_tables(Ct, Gt, ptab, s); });
         if (rc) return rc;
         float2* fl = reinterpret_cast<float2*>(ws + lay.fmap);
         float2* ql = reinterpret_cast<float2*>(spec1);
@@ -308,7 +308,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
         const size_t tslot = tr.iso_lane ? planes * MN / 2 : 0;   // float4 per slot
         for (int k = 0; k < maxit; ++k) {
             rc = ln.run(ADMM_K_PLANE, [&] {
-                return pk::launch_plane_iso(y, x_out, tables, kh > 0, spec0, st + (k > 0 ? (size_t)(k - 1) * tslot : 0),
+                return pk::launch_plane_iso(y, x_out, ptab, kh > 0, spec0, st + (k > 0 ? (size_t)(k - 1) * tslot : 0),
                                             st + (size_t)k * tslot, fl, ql, prm, k, maxit, planes, s);
             });
             if (rc) return rc;

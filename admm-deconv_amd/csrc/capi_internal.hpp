@@ -220,9 +220,11 @@ size_t multi_iso_rows(int K);
 admm::plane::Branches multi_branches(int P, int B, int nbr);
 
 // ---- launch sequencing (admm_launch.hip) ----
+// tables = false: the workspace already holds this call's twiddles, C / G tables and scalar block (a later plane
+// chunk of the same call through the same chunk workspace): the setup kernels are not launched again
 int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t planes, const float* h, int kh,
                 int kw, const admm::ScalarSrc& sc, int iso, int maxit, unsigned char* ws, const Layout& lay,
-                const Traj& tr, const admm_batch_reducer* red, int fwd_path);
+                const Traj& tr, const admm_batch_reducer* red, int fwd_path, bool tables = true);
 // everything run_backward does after validating the call and updating the recordings registry
 int launch_backward(int phases, const float* y, const float* x_bar, float* y_bar, float* h_bar, float* lambda_bar,
                     float* rho_bar, int M, int N, size_t planes, const float* h, int kh, int kw,
