@@ -51,6 +51,7 @@ __device__ __forceinline__ size_t map_plane(const Branches& br, int map, size_t 
     return map == kMapIn ? bo.in_plane : bo.out_plane;
 }
 constexpr int kSetupPsfLds = 4096;   // PSF taps the setup kernel stages in LDS (larger PSFs are read from global)
+constexpr int kSetupSplit = 4;       // setup_kernel lanes per spectral bin
 
 // XCD-aware block order (2-D grid (x, y) -> logical (x, y)).  Workgroups are dealt round-robin over
 // the 8 XCDs, each with its own L2 (MI355X_MICROARCH.md, workgroup dispatch): the bijective remap
@@ -126,7 +127,13 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
     const int nbins = H * N;
     const double inv_mn = 1.0 / ((double)M * (double)N);
     const int padd = (kh - 1) / 2, padr = (kw - 1) / 2;
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nbins; q += gridDim.x * blockDim.x) {
+    // kSetupSplit lanes per bin, each summing the PSF columns b = sub, sub + kSetupSplit, ...; the partial sums meet
+    // in a fixed xor-shuffle order.  (One lane per bin left 129 blocks at 256^2, each thread a 225-term dependent
+    // fp64 chain: 17.7 us of every c2 call.)
+    const int split = kh > 0 ? kSetupSplit : 1;
+    const int sub = threadIdx.x & (split - 1);
+    for (int qq = blockIdx.x * blockDim.x + threadIdx.x; qq < nbins * split; qq += gridDim.x * blockDim.x) {
+        const int q = qq / split;   // the split lanes of a bin are neighbours in one iteration
         const int kj = q / H;   // dim2 frequency
         const int k = q - kj * H;  // dim1 frequency 0..L
         double s2 = 1.0;
@@ -134,8 +141,9 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
             double re = 0.0, im = 0.0;
             // table indices (b kj) mod N and (a k) mod M advanced by one addition and one conditional
             // subtraction (kj < N, k < M) instead of an integer division per term: the same entries
-            int ib = 0;
-            for (int b = 0; b < kw; ++b) {
+            const int bstep = (int)(((long long)split * kj) % N);
+            int ib = (int)(((long long)sub * kj) % N);
+            for (int b = sub; b < kw; b += split) {
                 const double2 eb = tN[ib];
                 double gr = 0.0, gi = 0.0;
                 int ia = 0;
@@ -149,10 +157,16 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
                 }
                 re += gr * eb.x - gi * eb.y;
                 im += gr * eb.y + gi * eb.x;
-                ib += kj;
+                ib += bstep;
                 if (ib >= N) ib -= N;
             }
+#pragma unroll
+            for (int o = 1; o < kSetupSplit; o <<= 1) {
+                re += __shfl_xor(re, o);
+                im += __shfl_xor(im, o);
+            }
             s2 = re * re + im * im;
+            if (sub != 0) continue;
             if (SigT) SigT[q] = make_double2(re, im);   // top-left PSF spectrum (backward h_bar)
             // centred spectrum: Sigma_c = Sigma * exp(+2 pi i (padd k/M + padr kj/N)); store conj / (MN)
             const double2 pa = tM[(padd * k) % M];
@@ -163,6 +177,7 @@ __global__ __launch_bounds__(kThreads) void setup_kernel(float2* __restrict__ tw
             const double ci = re * pi - im * pr;
             Gt[q] = make_float2((float)(cr * inv_mn), (float)(ci * inv_mn));
         }
+        if (sub != 0) continue;
         const double sx = sinpi((double)kj / (double)N), sy = sinpi((double)k / (double)M);
         const double lap = 4.0 * sx * sx + 4.0 * sy * sy;   // |Lx|^2 + |Ly|^2 (ops.jl:35-36)
         Ct[q] = (float)(inv_mn / (s2 + (double)rho * lap));

@@ -264,7 +264,7 @@ int run_forward(Launcher& ln, const float* y, float* x_out, int M, int N, size_t
 
     if (tables) rc = ln.run(ADMM_K_SETUP, [&] {
         const size_t lds = (size_t)(M + N) * 16 + (kh * kw <= admm::kSetupPsfLds ? (size_t)kh * kw * 4 : 0);
-        const int nb = (int)(((size_t)(L + 1) * N + kThreads - 1) / kThreads);
+        const int nb = (int)(((size_t)(L + 1) * N * (kh > 0 ? admm::kSetupSplit : 1) + kThreads - 1) / kThreads);
         const int grid = nb < 1024 ? (nb < 1 ? 1 : nb) : 1024;
         set_lds(admm::setup_kernel, lds);
         hipLaunchKernelGGL(admm::setup_kernel, dim3(grid), dim3(kThreads), lds, s, twM, twN, Ct, Gt, h, kh, kw, M,
