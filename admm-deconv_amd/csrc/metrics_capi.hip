@@ -242,12 +242,17 @@ __device__ __forceinline__ void sobel(const float* s, int W, int r, int c, float
     gy = ((a00 - a20) + 2.f * (a01 - a21) + (a02 - a22)) * 0.125f;
 }
 
+// The hardware square root and reciprocal (1 ulp each, v_sqrt_f32 / v_rcp_f32) instead of the correctly rounded
+// sequences: den >= t > 0 and m >= 1e-8 are normal numbers, and the loss is held to 2e-5 of the fp64 oracle
+// (tests/test_gpu_metrics.py).
 __device__ __forceinline__ float gms_val(float mx, float my, float t, float al, float& dgdmx) {
     const float num = (2.f - al) * mx * my + t;
     const float den = mx * mx + my * my - al * mx * my + t;
-    dgdmx = ((2.f - al) * my * den - num * (2.f * mx - al * my)) / (den * den);
-    return num / den;
+    const float r = __builtin_amdgcn_rcpf(den);
+    dgdmx = ((2.f - al) * my * den - num * (2.f * mx - al * my)) * (r * r);
+    return num * r;
 }
+__device__ __forceinline__ float gmag(float gx, float gy) { return __builtin_amdgcn_sqrtf(gx * gx + gy * gy + 1e-16f); }
 
 // per-block (sum gms, sum gms^2).  (256 x 16 tiles -- 1.02x halo reads instead of 1.16x, 16 outputs per thread --
 // measured slower at c5's 960 planes of 256^2: forward 245 -> 260 us, backward 400 -> 568 us; not kept)
@@ -274,7 +279,7 @@ __global__ __launch_bounds__(kT) void gmsd_fwd_kernel(const float* __restrict__ 
         float gx, gy, hx, hy, dd;
         sobel(xs, W, r + 1, c + 1, gx, gy);
         sobel(ys, W, r + 1, c + 1, hx, hy);
-        const float mx = sqrtf(gx * gx + gy * gy + 1e-16f), my = sqrtf(hx * hx + hy * hy + 1e-16f);
+        const float mx = gmag(gx, gy), my = gmag(hx, hy);
         const float g = gms_val(mx, my, t, al, dd);
         s1 += g;
         s2 += (double)g * g;
@@ -307,9 +312,9 @@ __global__ __launch_bounds__(kT) void gmsd_bwd_kernel(const float* __restrict__ 
         float gx, gy, hx, hy, dg;
         sobel(xs, W, r + 1, c + 1, gx, gy);
         sobel(ys, W, r + 1, c + 1, hx, hy);
-        const float mx = sqrtf(gx * gx + gy * gy + 1e-16f), my = sqrtf(hx * hx + hy * hy + 1e-16f);
+        const float mx = gmag(gx, gy), my = gmag(hx, hy);
         const float g = gms_val(mx, my, t, al, dg);
-        const float gm = cf * (g - mu) * dg / mx;
+        const float gm = cf * (g - mu) * dg * __builtin_amdgcn_rcpf(mx);
         gbx[idx] = gm * gx;
         gby[idx] = gm * gy;
     }
