@@ -41,7 +41,7 @@ EXPORTS = ("admm_abi_version", "admm_last_error", "admm_tvd_workspace_bytes", "a
            "admm_metrics_workspace_bytes", "admm_gmsd_f32", "admm_gmsd_backward_f32", "admm_ssim_f32", "admm_mse_f32",
            "admm_profile_enable", "admm_profile_reset", "admm_profile_get",
            "admm_tvd_multi_workspace_bytes", "admm_tvd_forward_multi_dev_f32",
-           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths", "admm_query_forward_schedule",
+           "admm_tvd_backward_multi_recorded_dev_f32", "admm_copy_async", "admm_query_paths", "admm_query_forward_schedule", "admm_clamp_backward_f32",
            "admm_path_name", "admm_ipc_get_handle", "admm_ipc_open", "admm_ipc_close")
 
 # record flags (the want_hbar word of the record entry points) and multi-branch flags
@@ -163,6 +163,8 @@ def load():
     L.admm_ipc_close.argtypes = [c_void_p, c_int]
     L.admm_query_paths.restype = c_int
     L.admm_query_paths.argtypes = [c_int] * 4 + [ctypes.c_longlong] + [c_int] * 4 + [ctypes.POINTER(c_int)] * 2
+    L.admm_clamp_backward_f32.restype = c_int
+    L.admm_clamp_backward_f32.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_float, c_float, c_void_p]
     L.admm_query_forward_schedule.restype = c_int
     L.admm_query_forward_schedule.argtypes = [c_int] * 4 + [ctypes.c_longlong, ctypes.POINTER(ctypes.c_longlong),
                                               ctypes.POINTER(c_int)]

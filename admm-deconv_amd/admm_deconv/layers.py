@@ -38,12 +38,41 @@ def relu(x):
     return torch.relu(x)
 
 
+class _ClampFn(torch.autograd.Function):
+    """clamp(x, lo, hi) whose gradient is one HIP pass (admm_clamp_backward_f32: dy where lo <= x <= hi, as torch's
+    clamp) instead of autograd's compare / compare / and / where kernels."""
+
+    @staticmethod
+    def forward(ctx, x, lo, hi):
+        ctx.save_for_backward(x)
+        ctx.lo, ctx.hi = lo, hi
+        return torch.clamp(x, lo, hi)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        _lib.check(_lib.load().admm_clamp_backward_f32(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(),
+                                                       float(ctx.lo), float(ctx.hi),
+                                                       torch.cuda.current_stream(x.device).cuda_stream))
+        return dx, None, None
+
+
+def _clamp(x, lo, hi):
+    if isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.requires_grad:
+        return _ClampFn.apply(x, lo, hi)
+    return torch.clamp(x, lo, hi)
+
+
 def relu6(x):
-    return torch.clamp(x, 0.0, 6.0)
+    return _clamp(x, 0.0, 6.0)
 
 
 def relu1(x):
-    return torch.clamp(x, 0.0, 1.0)
+    """relu1(x) = min.(relu.(x), 1) (src/nets/net_build.jl:8)."""
+    return _clamp(x, 0.0, 1.0)
 
 
 def _nfan(dims):

@@ -18,6 +18,29 @@
 
 #include "capi_internal.hpp"
 
+namespace admm {
+// admm_clamp_backward_f32: four elements per thread (16-B accesses when the three pointers allow), grid-strided
+__global__ __launch_bounds__(256) void clamp_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                        float* dx, size_t n, float lo, float hi) {
+    const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dx)) &
+                      15) == 0;
+    for (size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (size_t)gridDim.x * 256 * 4) {
+        if (vec && i + 4 <= n) {
+            const float4 a = *reinterpret_cast<const float4*>(x + i);
+            const float4 g = *reinterpret_cast<const float4*>(dy + i);
+            float4 r;
+            r.x = (a.x >= lo && a.x <= hi) ? g.x : 0.0f;
+            r.y = (a.y >= lo && a.y <= hi) ? g.y : 0.0f;
+            r.z = (a.z >= lo && a.z <= hi) ? g.z : 0.0f;
+            r.w = (a.w >= lo && a.w <= hi) ? g.w : 0.0f;
+            *reinterpret_cast<float4*>(dx + i) = r;
+        } else {
+            for (size_t j = i; j < i + 4 && j < n; ++j) dx[j] = (x[j] >= lo && x[j] <= hi) ? dy[j] : 0.0f;
+        }
+    }
+}
+}  // namespace admm
+
 namespace admm_capi {
 
 thread_local std::string g_err;
@@ -654,6 +677,17 @@ int admm_profile_get(int kernel_class, double* total_ms, long long* launches) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     *total_ms = g_prof.ms[kernel_class];
     *launches = g_prof.n[kernel_class];
+    return ADMM_OK;
+}
+
+int admm_clamp_backward_f32(const float* x, const float* dy, float* dx, size_t n, float lo, float hi, void* stream) {
+    if (n == 0) return ADMM_OK;
+    if (!x || !dy || !dx) return fail(ADMM_E_INVALID, "admm_clamp_backward_f32: NULL pointer");
+    const size_t blocks = (n + 4 * 256 - 1) / (4 * 256);
+    hipLaunchKernelGGL(admm::clamp_bwd_kernel, dim3((unsigned)(blocks < 65535 * 8 ? blocks : 65535 * 8)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), x, dy, dx, n, lo, hi);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ADMM_E_HIP, "admm_clamp_backward_f32: %s", hipGetErrorString(e));
     return ADMM_OK;
 }
 

@@ -305,6 +305,11 @@ const char* admm_path_name(int path);
 int admm_query_forward_schedule(int M, int N, int iso, int kh, long long planes, long long* chunk_planes,
                                 int* streams);
 
+/* The gradient of the layers' clamp activations (sigma = relu1 = min.(relu.(x), 1), src/nets/net_build.jl:8, and
+ * relu6): dx[i] = (lo <= x[i] <= hi) ? dy[i] : 0 over n floats in one pass (autograd's form of the clamp is three
+ * kernels).  x, dy, dx device pointers (dx may be dy); ADMM_E_INVALID for NULL pointers when n > 0. */
+int admm_clamp_backward_f32(const float* x, const float* dy, float* dx, size_t n, float lo, float hi, void* stream);
+
 /* Output transport of the batch-sharded solve (BASELINE c3; the reference gathers nothing -- its batch
  * lives on one device, ops.jl:168-173): an asynchronous copy of `bytes` from src to dst on `stream`, both
  * device pointers, dst possibly memory of another GPU opened through a HIP IPC handle.  A plain

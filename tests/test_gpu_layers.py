@@ -208,3 +208,20 @@ def test_reference_demo_layer_forward_and_gradients(dev):
     assert rel(L.weight.grad.cpu().numpy().reshape(32, 32), hb0) < 1e-3
     assert abs(float(L.lam.grad) - lb0) <= 1e-3 * abs(lb0)
     assert abs(float(L.rho.grad) - rb0) <= 1e-3 * abs(rb0)
+
+
+@pytest.mark.parametrize("fn,hi", [(layers.relu1, 1.0), (layers.relu6, 6.0)], ids=["relu1", "relu6"])
+def test_clamp_activation_gradient_matches_autograd(dev, fn, hi):
+    """relu1 / relu6 backward through admm_clamp_backward_f32: bitwise torch.clamp's autograd, the ties at lo and hi
+    (gradient passed) and a length that is not a multiple of 4 included."""
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal(4099) * hi).astype(np.float32)
+    x[:6] = [0.0, hi, -0.0, np.nextafter(0, -1), np.nextafter(np.float32(hi), np.float32(2 * hi)), hi / 2]
+    g = torch.from_numpy(rng.standard_normal(4099).astype(np.float32)).to(dev)
+    a = torch.from_numpy(x).to(dev).requires_grad_(True)
+    b = torch.from_numpy(x).to(dev).requires_grad_(True)
+    ya, yb = fn(a), torch.clamp(b, 0.0, hi)
+    assert torch.equal(ya, yb)
+    ya.backward(g)
+    yb.backward(g)
+    assert torch.equal(a.grad, b.grad)
