@@ -44,6 +44,19 @@ static void sizes(void) {
     }
     size_t mw = 0;
     CHECK(admm_metrics_workspace_bytes(256, 256, 3, 4, 11, 1, &mw) == 0 && mw > 0);
+    /* the MALL-resident schedule (round 6): its workspace is n chunk workspaces, the query agrees with it */
+    long long chunk = 0;
+    int streams = 0;
+    size_t w4 = 0, w1 = 0, one = 0;
+    CHECK(admm_query_forward_schedule(512, 512, 0, 15, 768, &chunk, &streams) == ADMM_OK && chunk == 8 && streams == 4);
+    CHECK(admm_tvd_workspace_bytes(512, 512, 3, 256, 15, 15, 0, &w4) == ADMM_OK);
+    CHECK(admm_tvd_workspace_bytes(512, 512, 1, 8, 15, 15, 0, &one) == ADMM_OK);
+    CHECK(admm_set_option(ADMM_OPT_MALL_STREAMS, 1) == ADMM_OK);
+    CHECK(admm_tvd_workspace_bytes(512, 512, 3, 256, 15, 15, 0, &w1) == ADMM_OK);
+    CHECK(admm_query_forward_schedule(512, 512, 0, 15, 768, &chunk, &streams) == ADMM_OK && chunk == 768 && streams == 1);
+    CHECK(admm_set_option(ADMM_OPT_MALL_STREAMS, 4) == ADMM_OK);
+    CHECK(w4 >= 4 * one && w4 < w1);
+    CHECK(admm_query_forward_schedule(512, 512, 0, 15, 0, &chunk, &streams) == ADMM_E_INVALID);
 }
 
 static void validation(void) {
@@ -68,6 +81,13 @@ static void validation(void) {
     CHECK(admm_tvd_backward_recorded_f32((float*)fake, (float*)fake, (float*)fake, NULL, NULL, NULL, 64, 64, 1, 1,
                                          NULL, 0, 0, 0.1f, 1.0f, 0, 5, (float*)fake, fake + 4096, 1u << 30, NULL,
                                          NULL) == ADMM_E_INVALID);
+    /* round-6 entry points: validation before any device work */
+    CHECK(admm_clamp_backward_f32(NULL, (float*)fake, (float*)fake, 16, 0.f, 1.f, NULL) == ADMM_E_INVALID);
+    CHECK(admm_clamp_backward_f32(NULL, NULL, NULL, 0, 0.f, 1.f, NULL) == ADMM_OK);   /* n = 0: nothing to do */
+    CHECK(admm_gmsd_backward_f32((float*)fake, (float*)fake, 64, 64, 1, 1, 0.0026f, 0.f, NULL, NULL, fake, 1u << 20,
+                                 NULL) == ADMM_E_INVALID);
+    CHECK(admm_gmsd_backward_f32((float*)fake, (float*)fake, 64, 64, 1, 1, 0.0026f, 0.f, NULL, (float*)fake, fake, 8,
+                                 NULL) == ADMM_E_WORKSPACE);
     /* a long message must be truncated, not overflow the thread-local buffer */
     CHECK(admm_tvd_workspace_bytes(1 << 30, 1 << 30, 1, 1, 1 << 29, 1 << 29, 0, &ws) != ADMM_OK);
     CHECK(strlen(admm_last_error()) < 4096);
