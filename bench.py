@@ -592,6 +592,12 @@ def main():
         # s5); overlap = the kernels' event time per solve over the solve's wall time
         "schedule": {"chunk_planes": chunk, "streams": nstreams,
                      "overlap": round(sum(k["total_ms_per_solve"] for k in kernels.values()) / ms_per_step, 2)},
+        # with streams > 1: the dominant class's algorithmic bytes per solve over its share of the solve's wall time
+        # (its share of the summed event time) -- an estimate of the rate the concurrent launches reach together
+        "concurrent_estimate": None if nstreams <= 1 else {
+            "achieved_GBps": round(kernels[dom]["algorithmic_bytes_per_launch"] * kernels[dom]["launches_per_solve"]
+                                   / (ms_per_step * 1e-3 * kernels[dom]["total_ms_per_solve"]
+                                      / sum(k["total_ms_per_solve"] for k in kernels.values())) / 1e9, 1)},
         "whole_solve": {
             # the bytes of the path that ran (fused: plane_bytes_per_px; 2-pass: SURVEY s8d canonical)
             "algorithmic_bytes": alg_bytes,
