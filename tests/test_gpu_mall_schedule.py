@@ -56,6 +56,23 @@ def test_mall_schedule_bitwise_one_stream(dev, planes):
     assert_parity(x4[:2].cpu().numpy(), ref, what="mall schedule 512^2")
 
 
+def test_mall_schedule_c4_config_full_k(dev):
+    """The c4 configuration (512^2, 15x15 Gaussian PSF sigma 2.5, K = 50) over 96 planes -- 12 chunks of 8 on 4
+    streams: bitwise the one-stream solve, and planes of the first, a middle and the last chunk against the oracle."""
+    M, K, planes = 512, 50, 96
+    assert _lib.forward_schedule(M, M, False, 15, planes) == (8, 4)
+    h = synth.gaussian_psf(15, 2.5)
+    y_np = _batch(planes, M, h, g0=77)
+    y = torch.from_numpy(y_np).to(dev)
+    ht = torch.from_numpy(h).to(dev)
+    x4, _ = _solve(dev, y, ht, K, 4)
+    x1, _ = _solve(dev, y, ht, K, 1)
+    assert torch.equal(x4, x1)
+    pick = [0, 45, 95]   # chunk 0 (stream 0), chunk 5 (stream 1), chunk 11 (stream 3)
+    ref = oracle_solve(y_np[pick], LAM, RHO, h, False, K, "spectral", what="mall c4 K=50")
+    assert_parity(x4[pick].cpu().numpy(), ref, what="mall schedule c4 K=50")
+
+
 def test_mall_schedule_smooth_lengths(dev):
     """480 x 640 x 64 runs the smooth-length 2-pass kernels in 6-plane chunks on 4 streams: bitwise the whole batch."""
     N, M, B, K = 480, 640, 64, 4
