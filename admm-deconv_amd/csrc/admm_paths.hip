@@ -99,8 +99,9 @@ bool enough_planes(const PathIn& q, MinPlanesFor which) {
 // iteration, so every pass streams from HBM.  Chunks of ~224 MiB / n (8 planes at 512^2, n = 4) run all K
 // iterations with n of them in flight: their sets stay in the 256 MiB Infinity Cache, and the n streams overlap
 // each other's kernel tails.  tools/c4_chunk_probe.py, profiles/r06_c4_chunk_probe.jsonl: 81.8 -> 75.7 ms per c4
-// solve (8 planes x 4 streams; 16 x 2 77.2, 8 x 2 97.8: one or two small grids alone leave the chip idle; more
-// than 4 streams share the process's 4 hardware queues: 5-12 streams 97-149 ms, profiles/r06_c4_mall_streams_sweep.txt).
+// solve (8 planes x 4 streams; 16 x 2 77.2, 8 x 2 97.8: one or two small grids alone leave the chip idle; 5-12
+// streams 97-149 ms, profiles/r06_c4_mall_streams_sweep.txt -- their 4-5 plane chunks are too small: 4 x 4 97.0,
+// 5 x 4 85.3 ms; with 8 hardware queues 6 / 8 streams are slower still, profiles/r06_c4_hw_queues_probe.txt).
 // The smooth-length 2-pass kernels gain the same way (480 x 640 x 64 / 256 +5 / +7 %, 384^2 x 512 +11 %).
 ChunkPlan forward_chunks(int M, int N, size_t planes, bool iso, int fwd_path) {
     const size_t base = chunk_planes(planes, iso);
