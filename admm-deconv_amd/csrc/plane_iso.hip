@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void iso_norm_kernel(const float2* __restrict_
     } else {
         const float2* q = qpart + (size_t)i * br.ppb * kE + e;
         float2 a = make_float2(0.f, 0.f);
-#pragma unroll 4
+#pragma unroll 16   // (16 plane loads in flight per thread: the sums stay in the same order)
         for (int p = slice; p < br.ppb; p += 4) {
             const float2 v = q[(size_t)p * kE];
             a.x += v.x;
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void iso_radj_kernel(const float2* __restrict_
     constexpr size_t kE = 64 * kPT;
     const float2* q = rpart + (size_t)i * br.ppb * kE + e;
     float2 a = make_float2(0.f, 0.f);
-#pragma unroll 4
+#pragma unroll 16
     for (int p = slice; p < br.ppb; p += 4) {
         const float2 v = q[(size_t)p * kE];
         a.x += v.x;
