@@ -49,17 +49,8 @@ using rsrc_t = __amdgpu_buffer_rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-// cache-policy bits of the main-loop s / H^T y accesses (gfx950: 1 = sc0, 2 = nt, 16 = sc1);
-// experiment knobs, 0 = default policy
-#ifndef PLANE_AUX_LDS
-#define PLANE_AUX_LDS 0
-#endif
-#ifndef PLANE_AUX_LDH
-#define PLANE_AUX_LDH 0
-#endif
-#ifndef PLANE_AUX_ST
-#define PLANE_AUX_ST 0
-#endif
+// AUX: cache-policy bits of the access (gfx950: 1 = sc0, 2 = nt, 16 = sc1); every product access uses the default
+// policy (nt / sc0 / sc1 on the s and H^T y streams were measured, round 2: no gain)
 template <int AUX = 0>
 __device__ __forceinline__ float4 bld4(rsrc_t r, unsigned vo, unsigned so) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, AUX));
@@ -132,30 +123,13 @@ __device__ __forceinline__ void lds_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// PLANE_PROX selects the form of the prox arithmetic (same values for every finite input):
-//   0: clip = min(max(v, -tau), tau); w = |s| > tau ? s - 2 tau sign(s) : -s   (compare + select)
-//   1: clip = med3(v, -tau, tau) (one v_med3_f32); w = s - 2 clip(s) as one FMA (exact: s - 2s = -s,
-//      s - 2 tau sign(s) has one rounding either way)
-// Form 1 is the default since the store-data hazard it exposed is padded at build time (hazard_pad.py;
-// census green, c2 3.34 -> 3.29 ms per solve on one box).
-#ifndef PLANE_PROX
-#define PLANE_PROX 1
-#endif
-__device__ __forceinline__ float clip_tau(float v, float tau) {
-#if PLANE_PROX == 1
-    return __builtin_amdgcn_fmed3f(v, -tau, tau);
-#else
-    return fminf(fmaxf(v, -tau), tau);
-#endif
-}
+// The prox arithmetic: clip = med3(v, -tau, tau) (one v_med3_f32); w = s - 2 clip(s) as one FMA -- the same values
+// as min(max(v, -tau), tau) and |s| > tau ? s - 2 tau sign(s) : -s for every finite input (exact: s - 2s = -s,
+// s - 2 tau sign(s) has one rounding either way).  The compare / select form ran c2 at 3.34 ms, this one 3.29 ms
+// once the store-data hazard it exposed was padded at build time (hazard_pad.py; census green).
+__device__ __forceinline__ float clip_tau(float v, float tau) { return __builtin_amdgcn_fmed3f(v, -tau, tau); }
 // w = z - u with z = ST(s, tau) and u = s - z  (|s| > tau: s - 2 tau sign s, else -s)
-__device__ __forceinline__ float phi_tau(float s, float tau) {
-#if PLANE_PROX == 1
-    return fmaf(-2.0f, clip_tau(s, tau), s);
-#else
-    return fabsf(s) > tau ? s - copysignf(2.0f * tau, s) : -s;
-#endif
-}
+__device__ __forceinline__ float phi_tau(float s, float tau) { return fmaf(-2.0f, clip_tau(s, tau), s); }
 
 // Materialise every S register at a phase boundary.  Without it the compiler moves the tail of a line
 // transform past the next phase's LDS traffic in straight-line code, and the overlap of the two register
@@ -228,13 +202,9 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     // multipliers for this thread's 32 bins (coalesced, L2-resident), issued once v is dead so they do
     // not add to the register peak of the FFT
     sched_fence();
-    // MODE 1 (H^T y, once per solve) loads its complex multipliers in two halves of 16 (PLANE_GF_SPLIT):
-    // all 32 at once (64 VGPRs) set the PSF kernel's register peak and its allocation spilled inside the
-    // iteration loop as well
-#ifndef PLANE_GF_SPLIT
-#define PLANE_GF_SPLIT 1
-#endif
-    constexpr int NGF = (MODE == 1 && PLANE_GF_SPLIT) ? 16 : 32;
+    // MODE 1 (H^T y, once per solve) loads its complex multipliers in two halves of 16: all 32 at once (64 VGPRs)
+    // set the PSF kernel's register peak and its allocation spilled inside the iteration loop as well
+    constexpr int NGF = MODE == 1 ? 16 : 32;
     float cf[MODE == 0 ? 32 : 1];
     float2 gf[MODE == 1 ? 32 : 1];
 #pragma unroll
@@ -326,34 +296,23 @@ __device__ __forceinline__ void column_half(float2 (&S)[64], float2* colbuf, con
     lds_barrier();
 }
 
-// Line r -/+ 1 of the lane-pair layout is lane t -/+ 2.  PLANE_LANESHIFT 1: two whole-wave DPP shifts
-// (wave_shr:1 / wave_shl:1, VALU) per value; 0: __shfl_up/__shfl_down (a ds_bpermute, i.e. an LDS round
-// trip on the row phase's dependency chain).  Lanes 0,1 (up) / 62,63 (down) receive 0; the callers
-// overwrite them with the boundary lines from LDS.
-#ifndef PLANE_LANESHIFT
-#define PLANE_LANESHIFT 1
-#endif
+// Line r -/+ 1 of the lane-pair layout is lane t -/+ 2: two whole-wave DPP shifts (wave_shr:1 / wave_shl:1, VALU)
+// per value (a __shfl_up / __shfl_down is a ds_bpermute, an LDS round trip on the row phase's dependency chain:
+// c2 3.284 -> 3.259 ms).  Lanes 0,1 (up) / 62,63 (down) receive 0; the callers overwrite them with the boundary
+// lines from LDS.
 // v is pinned in place (the caller's own variable, which it reads again): pinning a by-value copy kept the
 // original alive beside it, one v_mov per shift
 __device__ __forceinline__ float lane_up2(float& vr) {   // lane i <- lane i - 2
     float v = vr;
-#if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true);
     return __int_as_float(__builtin_amdgcn_mov_dpp(a, 0x138, 0xF, 0xF, true));
-#else
-    return __shfl_up(v, 2);
-#endif
 }
 __device__ __forceinline__ float lane_down2(float& vr) {   // lane i <- lane i + 2
     float v = vr;
-#if PLANE_LANESHIFT
     __asm__ volatile("" : "+v"(v));
     const int a = __builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true);
     return __int_as_float(__builtin_amdgcn_mov_dpp(a, 0x130, 0xF, 0xF, true));
-#else
-    return __shfl_down(v, 2);
-#endif
 }
 
 // v(register n) = H^T y + rho D^T w, with w of registers n and n+1 (the partner lane's pixel after this
@@ -435,8 +394,8 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
     for (int g = 0; g < PD; ++g)
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
-            sor[g][j] = bld4<PLANE_AUX_LDS>(sp, t * 16, (g * CH + j) * kPT * 16);
-            hyr[g][j] = bld2<PLANE_AUX_LDH>(hp, t * 8, (g * CH + j) * kPT * 8);
+            sor[g][j] = bld4(sp, t * 16, (g * CH + j) * kPT * 16);
+            hyr[g][j] = bld2(hp, t * 8, (g * CH + j) * kPT * 8);
         }
     PLANE_STAMP(17);
     const float2* xbp = xb + (((w + 7) & 7) * 2 + hb) * 64;   // previous wave's last line
@@ -458,8 +417,8 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
                 __asm__ volatile("" ::"v"(sor[(g + PD) % (PD + 1)][j].x), "v"(sor[(g + PD) % (PD + 1)][j].y),
                                  "v"(sor[(g + PD) % (PD + 1)][j].z), "v"(sor[(g + PD) % (PD + 1)][j].w),
                                  "v"(hyr[(g + PD) % (PD + 1)][j].x), "v"(hyr[(g + PD) % (PD + 1)][j].y));
-                sor[(g + PD) % (PD + 1)][j] = bld4<PLANE_AUX_LDS>(sp, t * 16, ((g + PD) * CH + j) * kPT * 16);
-                hyr[(g + PD) % (PD + 1)][j] = bld2<PLANE_AUX_LDH>(hp, t * 8, ((g + PD) * CH + j) * kPT * 8);
+                sor[(g + PD) % (PD + 1)][j] = bld4(sp, t * 16, ((g + PD) * CH + j) * kPT * 16);
+                hyr[(g + PD) % (PD + 1)][j] = bld2(hp, t * 8, ((g + PD) * CH + j) * kPT * 8);
             }
         }
         if (n0 == 32) {   // half-way: x[32..63] in, v[0..30] out (x[31] still pending in S[31])
@@ -492,7 +451,7 @@ __device__ __forceinline__ void row_update(float2 (&S)[64], rsrc_t sp, rsrc_t sp
             float4 uo = make_float4(clip_tau(so.x, tau), clip_tau(so.y, tau), clip_tau(so.z, tau), clip_tau(so.w, tau));
             if (first) uo = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 s = make_float4(x.x - xu.x + uo.x, x.y - xu.y + uo.y, x.x - xl + uo.z, x.y - x.x + uo.w);
-            bst4<PLANE_AUX_ST>(sps, t * 16, n * kPT * 16, s);
+            bst4(sps, t * 16, n * kPT * 16, s);
             if constexpr (MASK) {
                 mbits |= mask_byte(s, tau) << (8 * (n & 3));
                 if ((n & 3) == 3) {
@@ -560,9 +519,6 @@ __device__ __forceinline__ void dbg_dump(float2* dbg, const float2 (&S)[64], int
     }
 }
 
-#ifndef PLANE_STAGE_INV
-#define PLANE_STAGE_INV 1
-#endif
 
 // grid = planes, block = 512, dynamic LDS = kLdsBytes.  K >= 1.
 // TRAJ: record the trajectory for the adjoint -- iteration k writes s_k to slot k-1 of `traj` (slot
@@ -619,9 +575,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
     const rsrc_t gfr = make_rsrc(Gf, PSF ? kTab * 8 : 0);
     if constexpr (PSF) {
         line_forward_pair(S, hb);
-#ifndef PLANE_NO_PIN
         pin_regs(S);
-#endif
         column_phase<1>(S, colbuf, tw, mir, cfr, C0b, gfr, G0b, t, hb);
         // = H^T y (the 1/(MN) is in Gf).  Staged as in the iterations (x[32..63] through per-thread LDS
         // slots, no barrier): the unstaged inverse's peak exceeds 256 VGPRs and spilled.
@@ -640,7 +594,7 @@ __global__ __launch_bounds__(kPT) void plane256_kernel(const float* __restrict__
         dbg_dump<DBG>(dbg, S, 4 * k - 3, t);
         // the last iteration keeps x in registers for the output; the others hand x[32..63] to the
         // row phase's LDS staging slots directly (no spill of the line inverse's peak)
-        constexpr bool kStage = (DBG == 0 || DBG == 3) && PLANE_STAGE_INV;
+        constexpr bool kStage = DBG == 0 || DBG == 3;
         if constexpr (!kStage) {
             line_inverse_pair(S, hb);
             dbg_dump<DBG>(dbg, S, 4 * k - 2, t);
